@@ -1,0 +1,192 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X Game-of-Life hot path (one JSON line on rank 0).
+
+A "step" is one generation (halo exchange + B3/S23 update) over the whole
+grid.  Default workload (BASELINE.json configs[4], weak scaling): a random
+50%-density 65536 x 65536 block per GPU, global grid
+(65536*dims0) x (65536*dims1) with dims = MPI_Dims_create(N); N = 1 is the
+65536^2 single-GPU configuration the 80%-of-HBM-roofline target is quoted on.
+Inputs are generated on the device (counter-based splitmix64, the same
+generator as oracle/life_oracle.c) and are resident in HBM before timing.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--kernel bit|byte]
+                  [--size 65536] [--workload weak|p46gun_big]
+
+N > 1 runs one process per GPU under torch.distributed.run: torch.distributed
+(gloo) carries the bootstrap (RCCL unique id), the barriers and the
+max-over-ranks timing; the halo data path is RCCL ncclSend/ncclRecv issued by
+liblife_mi355x.so itself.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "mpi-and-open-mp_amd"))
+
+import life_mi355x as lm  # noqa: E402  (loads liblife_mi355x.so before torch)
+
+lm._lib()
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--kernel", default="bit", choices=["bit", "byte"])
+    p.add_argument("--size", type=int, default=65536, help="per-GPU block edge (weak scaling)")
+    p.add_argument("--workload", default="weak", choices=["weak", "p46gun_big"])
+    p.add_argument("--seed", type=int, default=1)
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline sample budget")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(target_s: float):
+    """The CPU oracle (a restatement of the reference's row-strip life_step,
+    3-life/life_mpi.c:150-176, one OpenMP thread per strip) on a bounded
+    sample of the same workload: a random 50% 4096^2 grid."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    n = 4096
+    g = O.fill_random(n, n, 12345, 0.5)
+    t = time.perf_counter()
+    g = O.life_run(g, 1, threads)
+    one = max(time.perf_counter() - t, 1e-6)
+    gens = max(1, int(target_s / one))
+    t = time.perf_counter()
+    O.life_run(g, gens, threads)
+    dt = time.perf_counter() - t
+    res = {"value": n * n * gens / dt / 1e9, "unit": "Gcell-updates/s", "cores": threads, "kind": "port",
+           "sample": f"random 50% {n}x{n}, {gens} generations, oracle/life_oracle.c OpenMP row strips, "
+                     f"{dt:.1f} s"}
+    ref = O.ref_lib()
+    if ref is not None:  # the reference's own life_step (3-life/life2d.c), when built
+        m = 2048
+        g2 = O.fill_random(m, m, 12345, 0.5)
+        t = time.perf_counter()
+        O.ref_life_run(g2, 2)
+        dt2 = time.perf_counter() - t
+        res["reference_1core"] = {"value": m * m * 2 / dt2 / 1e9, "unit": "Gcell-updates/s",
+                                  "sample": f"random 50% {m}x{m}, 2 generations, reference life_step "
+                                            "(3-life/life2d.c:104-130, gcc -O2), 1 core"}
+    return res
+
+
+def load_traffic(kernel: str, size: int):
+    """HBM bytes per stencil launch from the committed rocprofv3 PMC summary."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        return t.get(f"{kernel}_{size}")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # noqa: F811
+
+        dist.init_process_group("gloo")
+    dims = lm.dims_create(world if world > 1 else a.gpus)
+    n_gpus = world if world > 1 else a.gpus
+
+    if a.workload == "p46gun_big":
+        steps_cfg, _, grid = lm.load_cfg(os.path.join(ROOT, "tests", "golden", "cfg", "p46gun_big.cfg"))
+        ny, nx = grid.shape
+        workload = "p46gun_big.cfg 500x500 (configs[1])"
+    else:
+        nx, ny = a.size * dims[0], a.size * dims[1]
+        grid = None
+        workload = f"random 50% {a.size}^2 per GPU, global {nx}x{ny} (configs[4] weak scaling)"
+
+    if world > 1:
+        uid = [lm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        life = lm.Life.for_rank(nx, ny, rank, world, uid[0], local_rank, kernel=a.kernel, dims=dims)
+    else:
+        life = lm.Life(nx, ny, shards=a.gpus, kernel=a.kernel, dims=dims)
+
+    if grid is not None:
+        life.upload(grid)
+    else:
+        life.fill_random(a.seed, 0.5)
+    life.step(a.warmup)
+    life.sync()
+
+    def barrier_sync():
+        # life.sync() = hipStreamSynchronize on every stream the library
+        # launches on (the only GPU work in this process); the barrier and
+        # max-over-ranks go through torch.distributed when N > 1.
+        life.sync()
+        if dist is not None:
+            dist.barrier()
+
+    life.set_timing(True)
+    barrier_sync()
+    t0 = time.perf_counter()
+    life.step(a.steps)
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    avg_ms, launches, bytes_per_launch = life.kernel_stats()
+    live = life.live_count()
+
+    if rank == 0:
+        cells = float(nx) * float(ny) * a.steps
+        value = cells / elapsed / 1e9
+        achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        traffic = load_traffic(a.kernel, a.size) if a.workload == "weak" else None
+        out = {
+            "metric": "Gcell-updates/sec at 1/2/4/8 MI355X + % of HBM roofline, bit-exact",
+            "value": round(value, 3),
+            "unit": "Gcell-updates/s",
+            "n_gpus": n_gpus,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32 (1 bit/cell)" if a.kernel == "bit" else "u8 (1 byte/cell)",
+            "data": "synthetic (device-side splitmix64 random, density 0.5)" if grid is None
+                    else "p46gun_big.cfg pattern",
+            "config": {"workload": workload, "nx": nx, "ny": ny, "dims": list(dims), "kernel": a.kernel,
+                       "parallelism": f"cartesian {dims[0]}x{dims[1]}", "live_cells_end": live},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel_avg_ms": round(avg_ms, 5), "kernel_launches": launches,
+                         "bytes_per_launch": bytes_per_launch},
+        }
+        if n_gpus == 1 and not a.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    life.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

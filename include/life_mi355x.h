@@ -1,0 +1,172 @@
+/*
+ * life_mi355x.h -- C ABI of the MI355X-native Game-of-Life hot path.
+ *
+ * Drop-in boundary for the reference kekoveca/MPI-and-Open-MP.  The reference
+ * has no library or FFI: its "operator interface" is the set of free functions
+ * on `life_t` in 6-cartesian/life_cart.c:39-49, called only from main()
+ * (life_cart.c:51-85).  Each entry point below names the reference function
+ * it replaces.  Plain pointers and sizes only; no torch or HIP types.
+ *
+ * Grid convention (same as the reference's ind(), life_cart.c:11): cells are
+ * 0/1, row-major, x fastest: cell (x, y) at grid[y*nx + x].  Indices are
+ * 64-bit (the reference overflows int beyond ~46340^2, life_cart.c:101).
+ *
+ * Errors: every int-returning call returns LIFE_OK (0) or a negative
+ * LIFE_E* code (the reference asserts or aborts via MPI_ERRORS_ARE_FATAL);
+ * life_strerror() names it.  Not thread-safe: one host thread owns a handle.
+ */
+#ifndef LIFE_MI355X_H
+#define LIFE_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LIFE_OK 0
+#define LIFE_EINVAL (-1)   /* bad argument (sizes, dims, empty block, ...) */
+#define LIFE_EHIP (-2)     /* HIP runtime error (message: life_last_error()) */
+#define LIFE_ERCCL (-3)    /* RCCL error */
+#define LIFE_ENOMEM (-4)   /* host or device allocation failed */
+#define LIFE_ESTATE (-5)   /* call not valid in this state */
+#define LIFE_EIO (-6)      /* file I/O or parse error (driver helpers) */
+
+/* Cell encoding / kernel family. */
+#define LIFE_KERNEL_BYTE 0 /* 1 byte per cell, SWAR byte stencil */
+#define LIFE_KERNEL_BIT 1  /* 1 bit per cell (32 cells/word), bit-sliced adder */
+
+/* Halo transport between shards. */
+#define LIFE_XPORT_AUTO 0  /* RCCL across processes/devices, LOCAL otherwise */
+#define LIFE_XPORT_RCCL 1  /* ncclSend/ncclRecv (xGMI) */
+#define LIFE_XPORT_LOCAL 2 /* device-to-device copies inside one process */
+
+typedef struct life_dev life_dev; /* opaque: device memory, streams, RCCL comms */
+
+/* ---------------------------------------------------------------- host only */
+
+/* decomposition(): block k of n cells over p parts, the last block takes the
+ * remainder.  Replaces life_cart.c:217-223 (and 5-gather/life_mpi.c:170-175). */
+void life_decomposition(int64_t n, int p, int k, int64_t *start, int64_t *stop);
+
+/* MPI_Dims_create(n, 2, {0,0}) as called in life_init (life_cart.c:117-118):
+ * dims[0] >= dims[1], as balanced as possible. 2->{2,1}, 4->{2,2}, 8->{4,2}. */
+void life_dims_create(int n, int dims[2]);
+
+/* One halo-exchange operation of a shard (replaces exchange_columns /
+ * exchange_rows / exchange_corners, life_cart.c:225-279, and the 1-D ring
+ * exchange of 5-gather/life_mpi.c:181-191).  Coordinates are the shard's
+ * LOCAL padded frame: owned cells x in [0,w), padded rows 1..h; the one-cell
+ * apron is x = -1 / x = w and padded rows 0 / h+1. */
+#define LIFE_HALO_SEND 0
+#define LIFE_HALO_RECV 1
+#define LIFE_HALO_FILL 2   /* periodic wrap inside the shard (dims[d] == 1) */
+#define LIFE_HALO_COLUMN 0 /* one cell per padded row: rows [first, first+count) at x = index */
+#define LIFE_HALO_ROW 1    /* contiguous cells x in [first, first+count) of padded row index */
+typedef struct {
+    int32_t phase; /* 0: x (columns) first, then 1: y (rows incl. corners) */
+    int32_t kind;  /* LIFE_HALO_SEND / RECV / FILL */
+    int32_t peer;  /* global shard rank, -1 for FILL */
+    int32_t what;  /* LIFE_HALO_COLUMN / LIFE_HALO_ROW */
+    int64_t index; /* column x, or padded row */
+    int64_t first; /* first padded row (column) or first cell x (row) */
+    int64_t count;
+} life_halo_op;
+
+/* Builds the per-generation halo plan of shard `rank` of a dims[0] x dims[1]
+ * periodic Cartesian partition (rank = c0*dims[1] + c1, dim 0 splits x, as
+ * MPI_Cart_create(reorder=0) at life_cart.c:119-121).  Writes up to max_ops
+ * ops in execution order and returns their number (or LIFE_EINVAL).  Sends
+ * to and receives from one peer are matched in issue order. */
+int life_halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank,
+                   life_halo_op *ops, int max_ops);
+
+/* Padded layout of a shard as allocated on the device: pitch and x-offset in
+ * bytes of a padded row, rows = h + 2.  For the bit encoding x-offset is the
+ * byte offset of the word holding cell 0. */
+typedef struct {
+    int64_t w, h;      /* owned block */
+    int64_t x0, y0;    /* global origin of the block */
+    int64_t pitch;     /* bytes per padded row */
+    int64_t xoff;      /* byte offset of owned cell x = 0 in a padded row */
+    int64_t rows;      /* h + 2 */
+    int64_t units;     /* 16-byte lanes per row the stencil walks */
+    int32_t kernel;    /* LIFE_KERNEL_* */
+    int32_t coords[2]; /* Cartesian coordinates of the shard */
+} life_layout;
+
+int life_layout_query(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int kernel,
+                      life_layout *out);
+
+const char *life_strerror(int err);
+const char *life_last_error(void); /* detail of the last LIFE_EHIP/ERCCL on this thread */
+
+/* ---------------------------------------------------------------- device */
+
+/* life_init (life_cart.c:92-144) minus the file parsing: sizes the global
+ * nx x ny periodic grid, splits it over `nshards` shards driven by THIS
+ * process (dims = life_dims_create(nshards)), one per visible device
+ * (shard i on device i % device_count), and allocates double-buffered padded
+ * blocks.  Transport AUTO: RCCL when every shard has its own device, LOCAL
+ * device copies otherwise (e.g. several logical shards on one GPU). */
+int life_dev_create(int64_t nx, int64_t ny, int nshards, int kernel, life_dev **out);
+
+/* Same with every knob: dims (0,0 = dims_create), transport. */
+int life_dev_create_ex(int64_t nx, int64_t ny, int nshards, int dims0, int dims1, int kernel,
+                       int transport, life_dev **out);
+
+/* One-process-per-GPU mode (torchrun / mpirun style): this process owns the
+ * single shard `rank` of `world` on `device`; `unique_id` (128 bytes) comes
+ * from life_get_unique_id() on rank 0, broadcast by the caller. */
+int life_get_unique_id(uint8_t unique_id[128]);
+int life_dev_create_rank(int64_t nx, int64_t ny, int kernel, int rank, int world, int dims0,
+                         int dims1, const uint8_t unique_id[128], int device, life_dev **out);
+
+/* The loaded cells of life_init (life_cart.c:104-109): `grid` is the full
+ * nx*ny host grid (nonzero = alive); each local shard takes its block.  Then
+ * fills the halos.  In rank mode every rank passes the full grid. */
+int life_dev_upload(life_dev *d, const uint8_t *grid);
+
+/* Device-side synthetic init (no host grid): cell(x,y) =
+ * (splitmix64(splitmix64(seed) ^ (y*nx+x)) >> 32) < thr32,
+ * splitmix64 the standard finaliser.  thr32 = density * 2^32. */
+int life_dev_fill_random(life_dev *d, uint64_t seed, uint32_t thr32);
+
+/* `generations` x (life_exchange + life_step): life_cart.c:73-74
+ * (replaces life_exchange :275-279 and life_step :189-215). Asynchronous. */
+int life_dev_step(life_dev *d, int64_t generations);
+
+/* life_collect (life_cart.c:281-305; MPI_Gather in 5-gather/life_mpi.c:177-179):
+ * device-side gather of every block to the root shard (global rank
+ * world-1, as the reference) and one copy into `grid` (nx*ny bytes, 0/1).
+ * In rank mode only the root writes `grid` (others may pass NULL). Blocking. */
+int life_dev_gather(life_dev *d, uint8_t *grid);
+
+/* Live cells over the whole grid (all ranks). Blocking. */
+int64_t life_dev_live_count(life_dev *d);
+
+int life_dev_sync(life_dev *d);
+int life_dev_layout(life_dev *d, int local_shard, life_layout *out);
+int life_dev_world(life_dev *d, int *world, int *dims0, int *dims1, int *nlocal, int *transport);
+
+/* Kernel timing for roofline reporting: when on, every stencil launch is
+ * bracketed by HIP events on the stream it runs on.  stats returns the mean
+ * device time of one stencil launch (ms), the number of launches, and the
+ * algorithmic HBM bytes one launch moves (1 B read + 1 B written per cell for
+ * BYTE, 2 bits for BIT, over the cells that launch updates). */
+int life_dev_set_timing(life_dev *d, int on);
+int life_dev_kernel_stats(life_dev *d, double *avg_ms, int64_t *launches, double *bytes_per_launch);
+
+/* Stencil tuning for the whole process, per kernel family (-1: both): rows
+ * each lane walks (16/32/64) and rows of loads kept in flight (2/4/8); 0
+ * keeps the current value.  Defaults come from measurement;
+ * LIFE_STEP_ROWS / LIFE_STEP_DEPTH override them at load time. */
+int life_tune(int kernel, int rows, int depth);
+
+/* life_free (life_cart.c:146-157). */
+void life_dev_destroy(life_dev *d);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LIFE_MI355X_H */

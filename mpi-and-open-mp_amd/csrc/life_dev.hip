@@ -1,0 +1,690 @@
+// life_dev.hip -- C-ABI runtime of the MI355X Game-of-Life hot path.
+//
+// One life_dev owns the shards this process drives.  Each shard = one block of
+// the dims[0] x dims[1] periodic Cartesian partition, double-buffered in HBM
+// with a one-cell apron, one HIP stream, and (RCCL transport) one RCCL
+// communicator rank.  Per generation (life_cart.c:73-74):
+//   life_step     -> stencil kernel(s) cur -> nxt            (life_kernels.hip)
+//   life_exchange -> phase x (columns), then phase y (rows of width+2),
+//                    each either a periodic fill inside the shard
+//                    (dims[d] == 1) or ncclSend/ncclRecv with the Cartesian
+//                    neighbours (replaces life_cart.c:225-279).
+// Overlap: the stencil is split into the boundary ring and the interior; the
+// ring runs first, the halo exchange of the NEW state runs on the comm stream
+// while the interior kernel runs on the compute stream.
+#include <rccl/rccl.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "life_kernels.h"
+#include "life_mi355x.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+void set_err(const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+}
+
+#define HIPCHK(expr)                                                                          \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess) {                                                               \
+            set_err("%s:%d %s: %s", __FILE__, __LINE__, #expr, hipGetErrorString(e_));        \
+            return e_ == hipErrorOutOfMemory ? LIFE_ENOMEM : LIFE_EHIP;                       \
+        }                                                                                     \
+    } while (0)
+
+#define NCCLCHK(expr)                                                                         \
+    do {                                                                                      \
+        ncclResult_t r_ = (expr);                                                             \
+        if (r_ != ncclSuccess) {                                                              \
+            set_err("%s:%d %s: %s", __FILE__, __LINE__, #expr, ncclGetErrorString(r_));       \
+            return LIFE_ERCCL;                                                                \
+        }                                                                                     \
+    } while (0)
+
+#define CHK(expr)                     \
+    do {                              \
+        int rc_ = (expr);             \
+        if (rc_ != LIFE_OK) return rc_; \
+    } while (0)
+
+struct TimedLaunch {
+    hipEvent_t a = nullptr, b = nullptr;
+};
+
+struct Shard {
+    int rank = 0;    // global shard rank (Cartesian rank, row-major coords)
+    int device = 0;
+    life_layout lay{};
+    uint8_t *buf[2] = {nullptr, nullptr};
+    int cur = 0;
+    hipStream_t stream = nullptr;  // compute
+    hipStream_t comm_stream = nullptr;
+    hipEvent_t ev_ring = nullptr, ev_halo = nullptr, ev_sync = nullptr;
+    ncclComm_t comm = nullptr;
+    uint8_t *col_send = nullptr, *col_recv = nullptr;  // 2*h bytes each
+    unsigned long long *d_count = nullptr;
+    uint8_t *sink = nullptr;  // stencil stores of lanes outside a region
+    std::vector<life_halo_op> plan;
+    std::vector<TimedLaunch> timers;
+    size_t timers_used = 0;
+};
+
+}  // namespace
+
+struct life_dev {
+    int64_t nx = 0, ny = 0;
+    int dims[2] = {1, 1};
+    int world = 1;
+    int kernel = LIFE_KERNEL_BYTE;
+    int transport = LIFE_XPORT_LOCAL;
+    bool rank_mode = false;
+    bool timing = false;
+    bool overlap = true;
+    std::vector<Shard> shards;
+    double acc_ms = 0.0;
+    int64_t acc_launches = 0;
+    double acc_bytes = 0.0;
+};
+
+namespace {
+
+life::Wrap wrap_of(const life_dev *d) { return life::Wrap{d->dims[0] == 1, d->dims[1] == 1}; }
+
+// Byte range of the row cells [first, first+count) of a padded row.
+void row_span(const life_layout &L, int64_t first, int64_t count, int64_t *off, int64_t *bytes) {
+    if (L.kernel == LIFE_KERNEL_BIT) {
+        const int64_t w0 = first >> 5, w1 = (first + count - 1) >> 5;  // floor division
+        *off = L.xoff + 4 * w0;
+        *bytes = 4 * (w1 - w0 + 1);
+    } else {
+        *off = L.xoff + first;
+        *bytes = count;
+    }
+}
+
+int shard_alloc(life_dev *d, Shard &s) {
+    HIPCHK(hipSetDevice(s.device));
+    const size_t bytes = (size_t)(s.lay.pitch * s.lay.rows);
+    for (int i = 0; i < 2; i++) {
+        HIPCHK(hipMalloc(&s.buf[i], bytes));
+        HIPCHK(hipMemset(s.buf[i], 0, bytes));
+    }
+    HIPCHK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&s.comm_stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&s.ev_ring, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&s.ev_halo, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&s.ev_sync, hipEventDisableTiming));
+    HIPCHK(hipMalloc(&s.col_send, (size_t)(2 * s.lay.h)));
+    HIPCHK(hipMalloc(&s.col_recv, (size_t)(2 * s.lay.h)));
+    HIPCHK(hipMalloc(&s.d_count, sizeof(unsigned long long)));
+    HIPCHK(hipMalloc(&s.sink, 1024));
+    life_halo_op ops[16];
+    const int n = life_halo_plan(d->nx, d->ny, d->dims[0], d->dims[1], s.rank, ops, 16);
+    if (n < 0) {
+        set_err("halo plan failed for shard %d", s.rank);
+        return LIFE_EINVAL;
+    }
+    s.plan.assign(ops, ops + n);
+    return LIFE_OK;
+}
+
+void shard_free(Shard &s) {
+    (void)hipSetDevice(s.device);
+    if (s.comm) (void)ncclCommDestroy(s.comm);
+    for (auto &t : s.timers) {
+        if (t.a) (void)hipEventDestroy(t.a);
+        if (t.b) (void)hipEventDestroy(t.b);
+    }
+    for (uint8_t *p : {s.buf[0], s.buf[1], s.col_send, s.col_recv, s.sink})
+        if (p) (void)hipFree(p);
+    if (s.d_count) (void)hipFree(s.d_count);
+    for (hipEvent_t e : {s.ev_ring, s.ev_halo, s.ev_sync})
+        if (e) (void)hipEventDestroy(e);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+    if (s.comm_stream) (void)hipStreamDestroy(s.comm_stream);
+}
+
+// All local shards' `which` streams wait for each other (LOCAL transport).
+int local_barrier(life_dev *d, bool comm) {
+    for (Shard &s : d->shards) {
+        HIPCHK(hipSetDevice(s.device));
+        HIPCHK(hipEventRecord(s.ev_sync, comm ? s.comm_stream : s.stream));
+    }
+    for (Shard &s : d->shards) {
+        HIPCHK(hipSetDevice(s.device));
+        for (Shard &t : d->shards)
+            if (&t != &s) HIPCHK(hipStreamWaitEvent(comm ? s.comm_stream : s.stream, t.ev_sync, 0));
+    }
+    return LIFE_OK;
+}
+
+Shard *find_local(life_dev *d, int rank) {
+    for (Shard &s : d->shards)
+        if (s.rank == rank) return &s;
+    return nullptr;
+}
+
+// Pointer + size of the k-th (0-based, per phase) send/recv buffer of op `o`.
+void op_buffer(const Shard &s, const life_halo_op &o, int slot, uint8_t *base, uint8_t **ptr, size_t *bytes) {
+    if (o.what == LIFE_HALO_COLUMN) {
+        uint8_t *st = o.kind == LIFE_HALO_SEND ? s.col_send : s.col_recv;
+        *ptr = st + (size_t)(slot * s.lay.h);
+        *bytes = (size_t)s.lay.h;
+    } else {
+        int64_t off, nb;
+        row_span(s.lay, o.first, o.count, &off, &nb);
+        *ptr = base + o.index * s.lay.pitch + off;
+        *bytes = (size_t)nb;
+    }
+}
+
+// One halo phase on buffer `which` of every local shard, on stream sel.
+int run_phase(life_dev *d, int phase, int which_rel, bool on_comm) {
+    auto stream_of = [&](Shard &s) { return on_comm ? s.comm_stream : s.stream; };
+    auto buf_of = [&](Shard &s) { return s.buf[s.cur ^ which_rel]; };
+    // An axis that is not partitioned (dims[d] == 1) has no halo: the stencil
+    // wraps it itself (life_kernels.hip, row_ptr / WRAPX).
+    if (d->dims[phase] == 1) return LIFE_OK;
+    if (phase == 0)
+        for (Shard &s : d->shards) {
+            HIPCHK(hipSetDevice(s.device));
+            HIPCHK(life::launch_pack_columns(s.lay, buf_of(s), s.col_send, stream_of(s)));
+        }
+    if (d->transport == LIFE_XPORT_RCCL) {
+        NCCLCHK(ncclGroupStart());
+        for (Shard &s : d->shards) {
+            int ns = 0, nr = 0;
+            for (const life_halo_op &o : s.plan) {
+                if (o.phase != phase) continue;
+                uint8_t *p;
+                size_t nb;
+                const int slot = o.kind == LIFE_HALO_SEND ? ns++ : nr++;
+                op_buffer(s, o, slot, buf_of(s), &p, &nb);
+                if (o.kind == LIFE_HALO_SEND)
+                    NCCLCHK(ncclSend(p, nb, ncclUint8, o.peer, s.comm, stream_of(s)));
+                else
+                    NCCLCHK(ncclRecv(p, nb, ncclUint8, o.peer, s.comm, stream_of(s)));
+            }
+        }
+        NCCLCHK(ncclGroupEnd());
+    } else {
+        CHK(local_barrier(d, on_comm));
+        for (Shard &s : d->shards) {
+            HIPCHK(hipSetDevice(s.device));
+            int nr = 0;
+            std::vector<int> seen_from;  // recvs from each peer so far
+            for (const life_halo_op &o : s.plan) {
+                if (o.phase != phase || o.kind != LIFE_HALO_RECV) continue;
+                const int slot = nr++;
+                int kth = 0;  // this is the kth recv from o.peer
+                for (int p : seen_from) kth += p == o.peer;
+                seen_from.push_back(o.peer);
+                Shard *src = find_local(d, o.peer);
+                if (!src) {
+                    set_err("LOCAL transport: peer %d not in this process", o.peer);
+                    return LIFE_ESTATE;
+                }
+                // matching send: the kth send from src to s.rank
+                int ns = 0, cnt = 0;
+                const life_halo_op *match = nullptr;
+                int match_slot = -1;
+                for (const life_halo_op &q : src->plan) {
+                    if (q.phase != phase || q.kind != LIFE_HALO_SEND) continue;
+                    const int qs = ns++;
+                    if (q.peer == s.rank && cnt++ == kth) {
+                        match = &q;
+                        match_slot = qs;
+                        break;
+                    }
+                }
+                if (!match) {
+                    set_err("LOCAL transport: no matching send %d->%d", o.peer, s.rank);
+                    return LIFE_ESTATE;
+                }
+                uint8_t *dp, *sp;
+                size_t dn, sn;
+                op_buffer(s, o, slot, buf_of(s), &dp, &dn);
+                op_buffer(*src, *match, match_slot, buf_of(*src), &sp, &sn);
+                if (dn != sn) {
+                    set_err("LOCAL transport: size mismatch %zu vs %zu", dn, sn);
+                    return LIFE_ESTATE;
+                }
+                if (src->device == s.device)
+                    HIPCHK(hipMemcpyAsync(dp, sp, dn, hipMemcpyDeviceToDevice, stream_of(s)));
+                else
+                    HIPCHK(hipMemcpyPeerAsync(dp, s.device, sp, src->device, dn, stream_of(s)));
+            }
+        }
+        CHK(local_barrier(d, on_comm));
+    }
+    if (phase == 0)
+        for (Shard &s : d->shards) {
+            HIPCHK(hipSetDevice(s.device));
+            HIPCHK(life::launch_unpack_columns(s.lay, buf_of(s), s.col_recv, stream_of(s)));
+        }
+    return LIFE_OK;
+}
+
+// Halo of buffer `which_rel` (0 = cur, 1 = nxt) on the compute streams.
+int exchange(life_dev *d, int which_rel, bool on_comm) {
+    CHK(run_phase(d, 0, which_rel, on_comm));
+    CHK(run_phase(d, 1, which_rel, on_comm));
+    return LIFE_OK;
+}
+
+// Launches one stencil region; when timing is on and `timed`, brackets it
+// with HIP events on the shard's compute stream and books its algorithmic
+// bytes (1 B read + 1 B written per BYTE cell, 2 bits per BIT cell).
+int launch_region(life_dev *d, Shard &s, const life::Region &r, bool timed) {
+    const uint8_t *in = s.buf[s.cur];
+    uint8_t *out = s.buf[s.cur ^ 1];
+    if (!d->timing || !timed) {
+        HIPCHK(life::launch_step(s.lay, in, out, s.sink, r, wrap_of(d), s.stream));
+        return LIFE_OK;
+    }
+    if (s.timers_used == s.timers.size()) {
+        TimedLaunch t;
+        HIPCHK(hipEventCreate(&t.a));
+        HIPCHK(hipEventCreate(&t.b));
+        s.timers.push_back(t);
+    }
+    TimedLaunch &t = s.timers[s.timers_used++];
+    HIPCHK(hipEventRecord(t.a, s.stream));
+    HIPCHK(life::launch_step(s.lay, in, out, s.sink, r, wrap_of(d), s.stream));
+    HIPCHK(hipEventRecord(t.b, s.stream));
+    const bool bit = s.lay.kernel == LIFE_KERNEL_BIT;
+    const int64_t cpu = bit ? 128 : 16;
+    const int64_t xa = r.u0 * cpu, xb = r.u1 * cpu < s.lay.w ? r.u1 * cpu : s.lay.w;
+    d->acc_bytes += (double)(xb - xa) * (double)(r.r1 - r.r0) * (bit ? 0.25 : 2.0);
+    return LIFE_OK;
+}
+
+int harvest_timers(life_dev *d) {
+    for (Shard &s : d->shards) {
+        HIPCHK(hipSetDevice(s.device));
+        for (size_t i = 0; i < s.timers_used; i++) {
+            HIPCHK(hipEventSynchronize(s.timers[i].b));
+            float ms = 0.f;
+            HIPCHK(hipEventElapsedTime(&ms, s.timers[i].a, s.timers[i].b));
+            d->acc_ms += ms;
+            d->acc_launches++;
+        }
+        s.timers_used = 0;
+    }
+    return LIFE_OK;
+}
+
+// One generation on every local shard.
+int generation(life_dev *d) {
+    const bool rx = d->dims[0] > 1, ry = d->dims[1] > 1;
+    if (!d->overlap || !(rx || ry)) {
+        for (Shard &s : d->shards) {
+            HIPCHK(hipSetDevice(s.device));
+            CHK(launch_region(d, s, life::Region{0, s.lay.units, 0, s.lay.h}, true));
+        }
+        for (Shard &s : d->shards) s.cur ^= 1;
+        return exchange(d, 0, false);
+    }
+    // Ring first (cells whose 3x3 neighbourhood reaches a partitioned axis'
+    // apron), then the halo of the new state on the comm stream, overlapped
+    // with the interior on the compute stream.
+    for (Shard &s : d->shards) {
+        HIPCHK(hipSetDevice(s.device));
+        const int64_t U = s.lay.units, H = s.lay.h;
+        const int64_t ra = ry ? 1 : 0, rb = ry ? H - 1 : H;  // interior rows
+        if (ry) {
+            CHK(launch_region(d, s, life::Region{0, U, 0, 1}, false));
+            if (H > 1) CHK(launch_region(d, s, life::Region{0, U, H - 1, H}, false));
+        }
+        if (rx && rb > ra) {
+            CHK(launch_region(d, s, life::Region{0, 1, ra, rb}, false));
+            if (U > 1) CHK(launch_region(d, s, life::Region{U - 1, U, ra, rb}, false));
+        }
+        HIPCHK(hipEventRecord(s.ev_ring, s.stream));
+        HIPCHK(hipStreamWaitEvent(s.comm_stream, s.ev_ring, 0));
+    }
+    CHK(exchange(d, 1, true));  // halo of nxt on the comm streams
+    for (Shard &s : d->shards) {
+        HIPCHK(hipSetDevice(s.device));
+        const int64_t U = s.lay.units, H = s.lay.h;
+        const int64_t ra = ry ? 1 : 0, rb = ry ? H - 1 : H;
+        const int64_t ua = rx ? 1 : 0, ub = rx ? U - 1 : U;
+        if (rb > ra && ub > ua) CHK(launch_region(d, s, life::Region{ua, ub, ra, rb}, true));
+        HIPCHK(hipEventRecord(s.ev_halo, s.comm_stream));
+        HIPCHK(hipStreamWaitEvent(s.stream, s.ev_halo, 0));
+    }
+    for (Shard &s : d->shards) s.cur ^= 1;
+    return LIFE_OK;
+}
+
+int create_common(life_dev *d, const std::vector<int> &ranks, const std::vector<int> &devices) {
+    for (size_t i = 0; i < ranks.size(); i++) {
+        d->shards.emplace_back();
+        Shard &s = d->shards.back();
+        s.rank = ranks[i];
+        s.device = devices[i];
+        const int rc = life_layout_query(d->nx, d->ny, d->dims[0], d->dims[1], s.rank, d->kernel, &s.lay);
+        if (rc != LIFE_OK) {
+            set_err("layout: nx=%lld ny=%lld dims=%dx%d rank %d kernel %d", (long long)d->nx,
+                    (long long)d->ny, d->dims[0], d->dims[1], s.rank, d->kernel);
+            return rc;
+        }
+    }
+    for (Shard &s : d->shards) CHK(shard_alloc(d, s));
+    return LIFE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *life_last_error(void) { return g_err.c_str(); }
+
+int life_dev_create_ex(int64_t nx, int64_t ny, int nshards, int dims0, int dims1, int kernel,
+                       int transport, life_dev **out) {
+    if (!out || nx <= 0 || ny <= 0 || nshards <= 0) return LIFE_EINVAL;
+    *out = nullptr;
+    int dims[2] = {dims0, dims1};
+    if (dims0 <= 0 || dims1 <= 0) life_dims_create(nshards, dims);
+    if (dims[0] * dims[1] != nshards) {
+        set_err("dims %dx%d != %d shards", dims[0], dims[1], nshards);
+        return LIFE_EINVAL;
+    }
+    int ndev = 0;
+    {
+        hipError_t e = hipGetDeviceCount(&ndev);
+        if (e != hipSuccess || ndev <= 0) {
+            set_err("no HIP device: %s", hipGetErrorString(e));
+            return LIFE_EHIP;
+        }
+    }
+    life_dev *d = new life_dev;
+    d->nx = nx;
+    d->ny = ny;
+    d->dims[0] = dims[0];
+    d->dims[1] = dims[1];
+    d->world = nshards;
+    d->kernel = kernel;
+    std::vector<int> ranks, devices;
+    for (int i = 0; i < nshards; i++) {
+        ranks.push_back(i);
+        devices.push_back(i % ndev);
+    }
+    const bool distinct = nshards <= ndev;
+    if (transport == LIFE_XPORT_AUTO) transport = (distinct && nshards > 1) ? LIFE_XPORT_RCCL : LIFE_XPORT_LOCAL;
+    if (transport == LIFE_XPORT_RCCL && !distinct) {
+        set_err("RCCL transport needs one device per shard (%d shards, %d devices)", nshards, ndev);
+        delete d;
+        return LIFE_EINVAL;
+    }
+    d->transport = transport;
+    int rc = create_common(d, ranks, devices);
+    if (rc == LIFE_OK && transport == LIFE_XPORT_RCCL && nshards > 1) {
+        std::vector<ncclComm_t> comms(nshards);
+        ncclResult_t r = ncclCommInitAll(comms.data(), nshards, devices.data());
+        if (r != ncclSuccess) {
+            set_err("ncclCommInitAll: %s", ncclGetErrorString(r));
+            rc = LIFE_ERCCL;
+        } else {
+            for (int i = 0; i < nshards; i++) d->shards[i].comm = comms[i];
+        }
+    }
+    if (rc == LIFE_OK && transport == LIFE_XPORT_LOCAL && nshards > 1) {
+        for (int a = 0; a < ndev && a < nshards; a++)
+            for (int b = 0; b < ndev && b < nshards; b++)
+                if (a != b) {
+                    (void)hipSetDevice(a);
+                    (void)hipDeviceEnablePeerAccess(b, 0);  // already-enabled is fine
+                }
+        (void)hipGetLastError();
+    }
+    if (rc != LIFE_OK) {
+        life_dev_destroy(d);
+        return rc;
+    }
+    *out = d;
+    return LIFE_OK;
+}
+
+int life_dev_create(int64_t nx, int64_t ny, int nshards, int kernel, life_dev **out) {
+    return life_dev_create_ex(nx, ny, nshards, 0, 0, kernel, LIFE_XPORT_AUTO, out);
+}
+
+int life_get_unique_id(uint8_t unique_id[128]) {
+    ncclUniqueId id;
+    NCCLCHK(ncclGetUniqueId(&id));
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    memcpy(unique_id, &id, sizeof id);
+    return LIFE_OK;
+}
+
+int life_dev_create_rank(int64_t nx, int64_t ny, int kernel, int rank, int world, int dims0, int dims1,
+                         const uint8_t unique_id[128], int device, life_dev **out) {
+    if (!out || nx <= 0 || ny <= 0 || world <= 0 || rank < 0 || rank >= world) return LIFE_EINVAL;
+    *out = nullptr;
+    int dims[2] = {dims0, dims1};
+    if (dims0 <= 0 || dims1 <= 0) life_dims_create(world, dims);
+    if (dims[0] * dims[1] != world) return LIFE_EINVAL;
+    life_dev *d = new life_dev;
+    d->nx = nx;
+    d->ny = ny;
+    d->dims[0] = dims[0];
+    d->dims[1] = dims[1];
+    d->world = world;
+    d->kernel = kernel;
+    d->rank_mode = true;
+    d->transport = LIFE_XPORT_RCCL;
+    int rc = create_common(d, {rank}, {device});
+    if (rc == LIFE_OK && world > 1) {
+        if (!unique_id) {
+            rc = LIFE_EINVAL;
+        } else {
+            ncclUniqueId id;
+            memcpy(&id, unique_id, sizeof id);
+            (void)hipSetDevice(device);
+            ncclResult_t r = ncclCommInitRank(&d->shards[0].comm, world, id, rank);
+            if (r != ncclSuccess) {
+                set_err("ncclCommInitRank(rank %d/%d): %s", rank, world, ncclGetErrorString(r));
+                rc = LIFE_ERCCL;
+            }
+        }
+    }
+    if (rc != LIFE_OK) {
+        life_dev_destroy(d);
+        return rc;
+    }
+    *out = d;
+    return LIFE_OK;
+}
+
+int life_dev_upload(life_dev *d, const uint8_t *grid) {
+    if (!d || !grid) return LIFE_EINVAL;
+    for (Shard &s : d->shards) {
+        const life_layout &L = s.lay;
+        HIPCHK(hipSetDevice(s.device));
+        uint8_t *stage = nullptr;
+        HIPCHK(hipMalloc(&stage, (size_t)(L.w * L.h)));
+        HIPCHK(hipMemcpy2DAsync(stage, (size_t)L.w, grid + L.y0 * d->nx + L.x0, (size_t)d->nx, (size_t)L.w,
+                                (size_t)L.h, hipMemcpyHostToDevice, s.stream));
+        HIPCHK(life::launch_import_block(L, stage, s.buf[s.cur], s.stream));
+        HIPCHK(hipStreamSynchronize(s.stream));
+        HIPCHK(hipFree(stage));
+    }
+    CHK(exchange(d, 0, false));
+    return life_dev_sync(d);
+}
+
+int life_dev_fill_random(life_dev *d, uint64_t seed, uint32_t thr32) {
+    if (!d) return LIFE_EINVAL;
+    uint64_t z = seed + 0x9E3779B97F4A7C15ull;  // key = splitmix64(seed)
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    const uint64_t key = z ^ (z >> 31);
+    for (Shard &s : d->shards) {
+        HIPCHK(hipSetDevice(s.device));
+        HIPCHK(life::launch_fill_random(s.lay, d->nx, key, thr32, s.buf[s.cur], s.stream));
+    }
+    CHK(exchange(d, 0, false));
+    return LIFE_OK;
+}
+
+int life_dev_step(life_dev *d, int64_t generations) {
+    if (!d || generations < 0) return LIFE_EINVAL;
+    for (int64_t g = 0; g < generations; g++) CHK(generation(d));
+    return LIFE_OK;
+}
+
+int life_dev_sync(life_dev *d) {
+    if (!d) return LIFE_EINVAL;
+    for (Shard &s : d->shards) {
+        HIPCHK(hipSetDevice(s.device));
+        HIPCHK(hipStreamSynchronize(s.stream));
+        HIPCHK(hipStreamSynchronize(s.comm_stream));
+    }
+    return LIFE_OK;
+}
+
+int life_dev_gather(life_dev *d, uint8_t *grid) {
+    if (!d) return LIFE_EINVAL;
+    const int root = d->world - 1;  // life_collect: cart rank of (dims0-1, dims1-1)
+    const bool have_root = find_local(d, root) != nullptr;
+    if (have_root && !grid) return LIFE_EINVAL;
+    CHK(life_dev_sync(d));
+    if (!d->rank_mode) {
+        // Every shard is in this process: each exports its block and copies it
+        // into place (parallel D2H over each device's own link).
+        for (Shard &s : d->shards) {
+            const life_layout &L = s.lay;
+            HIPCHK(hipSetDevice(s.device));
+            uint8_t *stage = nullptr;
+            HIPCHK(hipMalloc(&stage, (size_t)(L.w * L.h)));
+            HIPCHK(life::launch_export_block(L, s.buf[s.cur], stage, s.stream));
+            HIPCHK(hipMemcpy2DAsync(grid + L.y0 * d->nx + L.x0, (size_t)d->nx, stage, (size_t)L.w, (size_t)L.w,
+                                    (size_t)L.h, hipMemcpyDeviceToHost, s.stream));
+            HIPCHK(hipStreamSynchronize(s.stream));
+            HIPCHK(hipFree(stage));
+        }
+        return LIFE_OK;
+    }
+    // Rank mode: device-side gather to the root over RCCL, then D2H at the root.
+    Shard &s = d->shards[0];
+    HIPCHK(hipSetDevice(s.device));
+    int64_t maxb = 0;
+    for (int r = 0; r < d->world; r++) {
+        life_layout L;
+        CHK(life_layout_query(d->nx, d->ny, d->dims[0], d->dims[1], r, d->kernel, &L));
+        if (L.w * L.h > maxb) maxb = L.w * L.h;
+    }
+    uint8_t *stage = nullptr, *rstage = nullptr;
+    HIPCHK(hipMalloc(&stage, (size_t)(s.lay.w * s.lay.h)));
+    HIPCHK(life::launch_export_block(s.lay, s.buf[s.cur], stage, s.stream));
+    int rc = LIFE_OK;
+    if (s.rank != root) {
+        NCCLCHK(ncclSend(stage, (size_t)(s.lay.w * s.lay.h), ncclUint8, root, s.comm, s.stream));
+    } else {
+        HIPCHK(hipMemcpy2DAsync(grid + s.lay.y0 * d->nx + s.lay.x0, (size_t)d->nx, stage, (size_t)s.lay.w,
+                                (size_t)s.lay.w, (size_t)s.lay.h, hipMemcpyDeviceToHost, s.stream));
+        HIPCHK(hipMalloc(&rstage, (size_t)maxb));
+        for (int r = 0; r < d->world && rc == LIFE_OK; r++) {
+            if (r == root) continue;
+            life_layout L;
+            CHK(life_layout_query(d->nx, d->ny, d->dims[0], d->dims[1], r, d->kernel, &L));
+            NCCLCHK(ncclRecv(rstage, (size_t)(L.w * L.h), ncclUint8, r, s.comm, s.stream));
+            HIPCHK(hipMemcpy2DAsync(grid + L.y0 * d->nx + L.x0, (size_t)d->nx, rstage, (size_t)L.w, (size_t)L.w,
+                                    (size_t)L.h, hipMemcpyDeviceToHost, s.stream));
+            HIPCHK(hipStreamSynchronize(s.stream));
+        }
+    }
+    HIPCHK(hipStreamSynchronize(s.stream));
+    HIPCHK(hipFree(stage));
+    if (rstage) HIPCHK(hipFree(rstage));
+    return rc;
+}
+
+int64_t life_dev_live_count(life_dev *d) {
+    if (!d) return LIFE_EINVAL;
+    int64_t total = 0;
+    for (Shard &s : d->shards) {
+        HIPCHK(hipSetDevice(s.device));
+        HIPCHK(hipMemsetAsync(s.d_count, 0, sizeof(unsigned long long), s.stream));
+        HIPCHK(life::launch_live_count(s.lay, s.buf[s.cur], s.d_count, s.stream));
+        if (d->rank_mode && d->world > 1)
+            NCCLCHK(ncclAllReduce(s.d_count, s.d_count, 1, ncclUint64, ncclSum, s.comm, s.stream));
+        unsigned long long c = 0;
+        HIPCHK(hipMemcpyAsync(&c, s.d_count, sizeof c, hipMemcpyDeviceToHost, s.stream));
+        HIPCHK(hipStreamSynchronize(s.stream));
+        total += (int64_t)c;
+    }
+    return total;
+}
+
+int life_dev_layout(life_dev *d, int local_shard, life_layout *out) {
+    if (!d || !out || local_shard < 0 || local_shard >= (int)d->shards.size()) return LIFE_EINVAL;
+    *out = d->shards[local_shard].lay;
+    return LIFE_OK;
+}
+
+int life_dev_world(life_dev *d, int *world, int *dims0, int *dims1, int *nlocal, int *transport) {
+    if (!d) return LIFE_EINVAL;
+    if (world) *world = d->world;
+    if (dims0) *dims0 = d->dims[0];
+    if (dims1) *dims1 = d->dims[1];
+    if (nlocal) *nlocal = (int)d->shards.size();
+    if (transport) *transport = d->transport;
+    return LIFE_OK;
+}
+
+int life_dev_set_timing(life_dev *d, int on) {
+    if (!d) return LIFE_EINVAL;
+    CHK(harvest_timers(d));
+    d->timing = on != 0;
+    d->acc_ms = 0.0;
+    d->acc_launches = 0;
+    d->acc_bytes = 0.0;
+    return LIFE_OK;
+}
+
+int life_dev_kernel_stats(life_dev *d, double *avg_ms, int64_t *launches, double *bytes_per_launch) {
+    if (!d) return LIFE_EINVAL;
+    CHK(harvest_timers(d));
+    const double n = d->acc_launches ? (double)d->acc_launches : 1.0;
+    if (avg_ms) *avg_ms = d->acc_ms / n;
+    if (launches) *launches = d->acc_launches;
+    if (bytes_per_launch) *bytes_per_launch = d->acc_bytes / n;
+    return LIFE_OK;
+}
+
+int life_tune(int kernel, int rows, int depth) {
+    if ((rows && rows != 16 && rows != 32 && rows != 64) || (depth && depth != 2 && depth != 4 && depth != 8) ||
+        kernel < -1 || kernel > LIFE_KERNEL_BIT)
+        return LIFE_EINVAL;
+    life::set_step_tuning(kernel, rows, depth);
+    return LIFE_OK;
+}
+
+void life_dev_destroy(life_dev *d) {
+    if (!d) return;
+    for (Shard &s : d->shards) {
+        (void)hipSetDevice(s.device);
+        if (s.stream) (void)hipStreamSynchronize(s.stream);
+        if (s.comm_stream) (void)hipStreamSynchronize(s.comm_stream);
+    }
+    for (Shard &s : d->shards) shard_free(s);
+    delete d;
+}
+
+}  // extern "C"

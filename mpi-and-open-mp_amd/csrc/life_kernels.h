@@ -1,0 +1,71 @@
+// life_kernels.h -- host-side launchers of the gfx950 Game-of-Life kernels.
+//
+// All launchers are asynchronous on `s` and return the hipError_t of the
+// launch.  Buffers are the padded shard layout of life_layout (see
+// include/life_mi355x.h and DESIGN.md "Data layout in HBM").
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "life_mi355x.h"
+
+namespace life {
+
+// Region of owned cells a stencil launch updates: 16-byte units [u0,u1) of
+// every padded row, owned rows [r0,r1) (0-based, padded row = r + 1).
+struct Region {
+    int64_t u0, u1, r0, r1;
+};
+
+// Kernel arguments of one stencil launch (by value).
+struct StepArgs {
+    const uint8_t *in;
+    uint8_t *out;
+    uint8_t *sink;  // >= 1 KiB scratch: stores of lanes outside the region land here
+    int64_t pitch, xoff, units, w, h;
+    int64_t u0, u1, r0, r1, nbx;
+    int32_t wrapy;
+};
+
+// Wrap flags: a periodic axis that lies entirely inside the shard (dims[d]
+// == 1) is wrapped by the stencil itself (no apron, no fill kernel); the
+// apron of a partitioned axis must hold the neighbours' cells.
+struct Wrap {
+    bool x, y;
+};
+
+// One generation over `reg`: reads `in`, writes `out`.
+hipError_t launch_step(const life_layout &L, const uint8_t *in, uint8_t *out, uint8_t *sink,
+                       const Region &reg, Wrap wrap, hipStream_t s);
+
+// Tuning knobs of the stencil (rows per lane, rows of loads in flight);
+// defaults chosen by measurement, overridable by LIFE_STEP_ROWS / LIFE_STEP_DEPTH.
+struct StepTuning {
+    int rows, depth;
+};
+StepTuning step_tuning(bool bit);
+void set_step_tuning(int kernel, int rows, int depth);  // kernel -1: both
+
+// Column halo staging: pack writes column w-1 to stage[0..h) and column 0 to
+// stage[h..2h) (1 byte 0/1 per row); unpack writes stage[0..h) to x = -1 and
+// stage[h..2h) to x = w.
+hipError_t launch_pack_columns(const life_layout &L, const uint8_t *buf, uint8_t *stage,
+                               hipStream_t s);
+hipError_t launch_unpack_columns(const life_layout &L, uint8_t *buf, const uint8_t *stage,
+                                 hipStream_t s);
+
+// Dense w*h byte block (row pitch w) <-> padded encoded buffer.
+hipError_t launch_import_block(const life_layout &L, const uint8_t *dense, uint8_t *buf,
+                               hipStream_t s);
+hipError_t launch_export_block(const life_layout &L, const uint8_t *buf, uint8_t *dense,
+                               hipStream_t s);
+
+// Counter-based synthetic init of the owned cells (global indices).
+hipError_t launch_fill_random(const life_layout &L, int64_t nx, uint64_t key, uint32_t thr32,
+                              uint8_t *buf, hipStream_t s);
+
+// Adds the number of live owned cells to *count.
+hipError_t launch_live_count(const life_layout &L, const uint8_t *buf,
+                             unsigned long long *count, hipStream_t s);
+
+}  // namespace life

@@ -1,0 +1,553 @@
+// life_kernels.hip -- gfx950 (CDNA4) kernels of the Game-of-Life hot path.
+//
+// Replaces the reference's life_step (6-cartesian/life_cart.c:189-215, the
+// same body as 3-life/life2d.c:104-130): B3/S23 on a periodic grid.  The
+// reference reads 9 ints through a modulo-wrapping ind() per cell; here every
+// shard is a padded block whose one-cell apron holds the periodic / remote
+// neighbours (filled by the halo phase), so the stencil is branch-free.
+//
+// Stencil mapping (both encodings): one lane owns a 16-byte unit of a row and
+// walks R consecutive rows down, keeping the horizontal 3-sums of rows y-1,
+// y, y+1 in registers (vertical reuse in registers, no LDS round trip).  The
+// horizontal neighbours of a unit's edge cells come from lanes +-1 by DPP
+// wave shifts (v_mov_b32_dpp wave_shr/wave_shl); lane 0 / lane 63 fetch the
+// one dword beyond the wave's span themselves.  HBM traffic is one read and
+// one write of each cell's encoding plus 2/R of re-read halo rows.
+//
+//  * ByteEnc: 1 byte per cell.  SWAR on 4 cells per dword: horizontal sum via
+//    v_alignbyte, 9-cell sum n9 <= 9 per byte, rule ((n9 - c) | c) == 3.
+//  * BitEnc: 1 bit per cell, 32 cells per dword, x = bit 0 upward.
+//    Horizontal (L,C,R) full adder -> 2-bit sum per row; three rows add to
+//    n9 = u0 + 2*S; alive' = (n9 == 3) | (alive & n9 == 4).
+#include "life_kernels.h"
+
+#include <stdlib.h>
+
+namespace life {
+namespace {
+
+constexpr int kBlock = 256;  // 4 waves of 64
+
+__device__ __forceinline__ uint32_t from_left(uint32_t old, uint32_t v) {
+    // lane i <- lane i-1 (wave_shr:1); lane 0 keeps `old`.
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t from_right(uint32_t old, uint32_t v) {
+    // lane i <- lane i+1 (wave_shl:1); lane 63 keeps `old`.
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x130, 0xf, 0xf, false);
+}
+
+// ------------------------------------------------------------------ encodings
+struct ByteEnc {
+    static constexpr int64_t kCellsPerUnit = 16;
+    static constexpr uint32_t kCell0 = 0xFFu;  // cell 0 of a dword
+    static __device__ __forceinline__ int64_t dword_of(int64_t x) { return x >> 2; }
+    static __device__ __forceinline__ uint32_t pos_in_dword(int64_t x) { return 8u * (uint32_t)(x & 3); }
+    static __device__ __forceinline__ uint32_t top_shift(int64_t x) { return 24u - pos_in_dword(x); }
+    struct H {
+        uint32_t v[4];
+    };
+    // Horizontal 3-sum (x-1, x, x+1) of 16 byte cells; l / r: dword left of
+    // d.x and dword right of d.w.
+    static __device__ __forceinline__ H hsum(uint4 d, uint32_t l, uint32_t r) {
+        H h;
+        h.v[0] = d.x + __builtin_amdgcn_alignbyte(d.x, l, 3) + __builtin_amdgcn_alignbyte(d.y, d.x, 1);
+        h.v[1] = d.y + __builtin_amdgcn_alignbyte(d.y, d.x, 3) + __builtin_amdgcn_alignbyte(d.z, d.y, 1);
+        h.v[2] = d.z + __builtin_amdgcn_alignbyte(d.z, d.y, 3) + __builtin_amdgcn_alignbyte(d.w, d.z, 1);
+        h.v[3] = d.w + __builtin_amdgcn_alignbyte(d.w, d.z, 3) + __builtin_amdgcn_alignbyte(r, d.w, 1);
+        return h;
+    }
+    static __device__ __forceinline__ uint32_t rule1(uint32_t n9, uint32_t c) {
+        const uint32_t m = (n9 - c) | c;                          // n8 | alive, per byte <= 9
+        const uint32_t t = m ^ 0x03030303u;                       // 0 where m == 3
+        const uint32_t nz = (t + 0x7F7F7F7Fu) & 0x80808080u;      // 0x80 where t != 0
+        return (nz ^ 0x80808080u) >> 7;
+    }
+    static __device__ __forceinline__ uint4 rule(const H &a, const H &b, const H &c, uint4 v) {
+        uint4 o;
+        o.x = rule1(a.v[0] + b.v[0] + c.v[0], v.x);
+        o.y = rule1(a.v[1] + b.v[1] + c.v[1], v.y);
+        o.z = rule1(a.v[2] + b.v[2] + c.v[2], v.z);
+        o.w = rule1(a.v[3] + b.v[3] + c.v[3], v.w);
+        return o;
+    }
+};
+
+struct BitEnc {
+    static constexpr int64_t kCellsPerUnit = 128;
+    static constexpr uint32_t kCell0 = 1u;
+    static __device__ __forceinline__ int64_t dword_of(int64_t x) { return x >> 5; }
+    static __device__ __forceinline__ uint32_t pos_in_dword(int64_t x) { return (uint32_t)(x & 31); }
+    static __device__ __forceinline__ uint32_t top_shift(int64_t x) { return 31u - pos_in_dword(x); }
+    struct H {
+        uint32_t s0[4], s1[4];
+    };
+    static __device__ __forceinline__ void fa(uint32_t L, uint32_t C, uint32_t R, uint32_t &s0,
+                                              uint32_t &s1) {
+        const uint32_t t = L ^ C;
+        s0 = t ^ R;
+        s1 = (t & R) | (~t & L);  // majority (v_bfi_b32)
+    }
+    static __device__ __forceinline__ H hsum(uint4 d, uint32_t l, uint32_t r) {
+        H h;
+        fa(__builtin_amdgcn_alignbit(d.x, l, 31), d.x, __builtin_amdgcn_alignbit(d.y, d.x, 1), h.s0[0], h.s1[0]);
+        fa(__builtin_amdgcn_alignbit(d.y, d.x, 31), d.y, __builtin_amdgcn_alignbit(d.z, d.y, 1), h.s0[1], h.s1[1]);
+        fa(__builtin_amdgcn_alignbit(d.z, d.y, 31), d.z, __builtin_amdgcn_alignbit(d.w, d.z, 1), h.s0[2], h.s1[2]);
+        fa(__builtin_amdgcn_alignbit(d.w, d.z, 31), d.w, __builtin_amdgcn_alignbit(r, d.w, 1), h.s0[3], h.s1[3]);
+        return h;
+    }
+    static __device__ __forceinline__ uint32_t rule1(uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1,
+                                                     uint32_t c0, uint32_t c1, uint32_t alive) {
+        uint32_t u0, k0, v0, v1;
+        fa(a0, b0, c0, u0, k0);  // bit-0 column: u0 + 2*k0
+        fa(a1, b1, c1, v0, v1);  // bit-1 column: v0 + 2*v1 (weight 2)
+        // n9 = u0 + 2*S, S = v0 + k0 + 2*v1 = p + 2*(q + v1)
+        const uint32_t p = v0 ^ k0, q = v0 & k0;
+        const uint32_t eq1 = p & ~(v1 | q);   // S == 1
+        const uint32_t eq2 = ~p & (v1 ^ q);   // S == 2
+        return (u0 & eq1) | (~u0 & alive & eq2);  // n9 == 3  |  (alive & n9 == 4)
+    }
+    static __device__ __forceinline__ uint4 rule(const H &a, const H &b, const H &c, uint4 v) {
+        uint4 o;
+        o.x = rule1(a.s0[0], a.s1[0], b.s0[0], b.s1[0], c.s0[0], c.s1[0], v.x);
+        o.y = rule1(a.s0[1], a.s1[1], b.s0[1], b.s1[1], c.s0[1], c.s1[1], v.y);
+        o.z = rule1(a.s0[2], a.s1[2], b.s0[2], b.s1[2], c.s0[2], c.s1[2], v.z);
+        o.w = rule1(a.s0[3], a.s1[3], b.s0[3], b.s1[3], c.s0[3], c.s1[3], v.w);
+        return o;
+    }
+};
+
+// ------------------------------------------------------------------ stencil
+// Per-lane constants of one stencil launch.  Every load is unconditional (a
+// lane right of the row reads a clamped, in-pitch unit) and every store
+// goes somewhere (a lane that must not write redirects to `sink` with row
+// stride 0), so a lane's whole strip is ONE basic block and the prefetch ring
+// below really keeps D rows of loads in flight.
+struct Lane {
+    const uint8_t *in;
+    int64_t pitch, h;
+    int64_t off;        // byte offset of the (clamped) unit in a padded row
+    int64_t exoff;      // extra dword: left (lane 0), right (lane 63), wrap-left (unit 0)
+    uint32_t exshift;   // wrap-left: move cell w-1 to the top position of the dword
+    int64_t xoff;       // word 0 of a row (wrap-right source)
+    uint4 pmask;        // wrap-right: where cell w sits inside this unit (last unit only)
+    uint32_t pshift;    //   ... its bit/byte position within that dword
+    bool pright;        // wrap-right: cell w is the right extra (w % cells_per_unit == 0)
+    bool wrapy;
+};
+
+__device__ __forceinline__ const uint8_t *row_ptr(const Lane &c, int64_t p) {
+    // padded row p in [0, h+1]; with a periodic y axis inside the shard the
+    // apron rows are the opposite owned rows (ind() wrap, life_cart.c:11).
+    if (c.wrapy) p = p == 0 ? c.h : (p == c.h + 1 ? 1 : p);
+    return c.in + p * c.pitch;
+}
+
+struct RowData {
+    uint4 d;
+    uint32_t ex, e0;
+};
+
+template <bool WRAPX>
+__device__ __forceinline__ RowData load_row(const Lane &c, int64_t p) {
+    const uint8_t *row = row_ptr(c, p);
+    RowData r;
+    r.d = *reinterpret_cast<const uint4 *>(row + c.off);
+    r.ex = *reinterpret_cast<const uint32_t *>(row + c.exoff);
+    r.e0 = WRAPX ? *reinterpret_cast<const uint32_t *>(row + c.xoff) : 0u;  // one address per wave
+    return r;
+}
+
+template <class E, bool WRAPX>
+__device__ __forceinline__ typename E::H row_sum(const Lane &c, RowData &r) {
+    uint32_t ex = r.ex << c.exshift;
+    uint32_t right = from_right(ex, r.d.x);
+    if (WRAPX) {
+        // the cell right of w-1 is cell 0 of the row (periodic x inside the shard)
+        const uint32_t c0 = (r.e0 & E::kCell0) << c.pshift;
+        r.d.x = (r.d.x & ~c.pmask.x) | (c0 & c.pmask.x);
+        r.d.y = (r.d.y & ~c.pmask.y) | (c0 & c.pmask.y);
+        r.d.z = (r.d.z & ~c.pmask.z) | (c0 & c.pmask.z);
+        r.d.w = (r.d.w & ~c.pmask.w) | (c0 & c.pmask.w);
+        right = c.pright ? r.e0 : right;
+    }
+    return E::hsum(r.d, from_left(ex, r.d.w), right);
+}
+
+// N output rows starting at owned row ys (padded rows ys .. ys+N+1 are read),
+// D rows of loads kept in flight.
+template <class E, int N, int D, bool WRAPX>
+__device__ __forceinline__ void strip_full(const Lane &c, int64_t ys, uint8_t *dst, int64_t spitch) {
+    static_assert(D <= N + 2, "prefetch deeper than the strip");
+    RowData q[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) q[k] = load_row<WRAPX>(c, ys + k);
+    typename E::H hp, hc;
+    uint4 cc;
+#pragma unroll
+    for (int k = 0; k < N + 2; ++k) {
+        RowData r = q[k % D];
+        if (k + D < N + 2) q[k % D] = load_row<WRAPX>(c, ys + k + D);
+        const typename E::H hn = row_sum<E, WRAPX>(c, r);
+        if (k == 0) {
+            hp = hn;
+        } else if (k == 1) {
+            hc = hn;
+            cc = r.d;
+        } else {
+            *reinterpret_cast<uint4 *>(dst) = E::rule(hp, hc, hn, cc);
+            dst += spitch;
+            hp = hc;
+            hc = hn;
+            cc = r.d;
+        }
+    }
+}
+
+template <class E, bool WRAPX>
+__device__ __forceinline__ void strip_tail(const Lane &c, int64_t ys, int n, uint8_t *dst, int64_t spitch) {
+    RowData r = load_row<WRAPX>(c, ys);
+    typename E::H hp = row_sum<E, WRAPX>(c, r);
+    r = load_row<WRAPX>(c, ys + 1);
+    typename E::H hc = row_sum<E, WRAPX>(c, r);
+    uint4 cc = r.d;
+#pragma unroll 1
+    for (int i = 0; i < n; ++i) {
+        r = load_row<WRAPX>(c, ys + 2 + i);
+        const typename E::H hn = row_sum<E, WRAPX>(c, r);
+        *reinterpret_cast<uint4 *>(dst) = E::rule(hp, hc, hn, cc);
+        dst += spitch;
+        hp = hc;
+        hc = hn;
+        cc = r.d;
+    }
+}
+
+template <class E, int R, int D, bool WRAPX>
+__global__ __launch_bounds__(kBlock) void step_kernel(StepArgs a) {
+    const int64_t bx = blockIdx.x % a.nbx, by = blockIdx.x / a.nbx;
+    const int lane = threadIdx.x & 63;
+    const int64_t wbase = a.u0 + (bx * (kBlock / 64) + (threadIdx.x >> 6)) * 64;
+    if (wbase >= a.u1) return;  // the whole wave is right of the region
+    const int64_t ys = a.r0 + by * R;
+    const int64_t u = wbase + lane;
+    const int64_t uc = u < a.units ? u : a.units;  // unit `units` is in-pitch: right-neighbour provider
+    Lane c;
+    c.in = a.in;
+    c.pitch = a.pitch;
+    c.h = a.h;
+    c.wrapy = a.wrapy != 0;
+    c.xoff = a.xoff;
+    c.off = a.xoff + 16 * uc;
+    c.exoff = c.off;
+    c.exshift = 0;
+    if (lane == 0) c.exoff = c.off - 4;
+    if (lane == 63 && u < a.units) c.exoff = c.off + 16;
+    c.pmask = make_uint4(0u, 0u, 0u, 0u);
+    c.pshift = 0;
+    c.pright = false;
+    if (WRAPX) {
+        if (u == 0) {  // left of cell 0 is cell w-1
+            const int64_t wl = a.w - 1;
+            c.exoff = a.xoff + E::dword_of(wl) * 4;
+            c.exshift = E::top_shift(wl);
+        }
+        if (u == a.units - 1) {  // right of cell w-1 is cell 0
+            const int64_t q = a.w - (a.units - 1) * E::kCellsPerUnit;  // 1 .. kCellsPerUnit
+            if (q == E::kCellsPerUnit) {
+                c.pright = true;
+            } else {
+                const int comp = (int)E::dword_of(q);
+                const uint32_t m = E::kCell0 << E::pos_in_dword(q);
+                c.pshift = E::pos_in_dword(q);
+                c.pmask.x = comp == 0 ? m : 0u;
+                c.pmask.y = comp == 1 ? m : 0u;
+                c.pmask.z = comp == 2 ? m : 0u;
+                c.pmask.w = comp == 3 ? m : 0u;
+            }
+        }
+    }
+    const bool st = u < a.u1;
+    uint8_t *dst = st ? a.out + (ys + 1) * a.pitch + a.xoff + 16 * u : a.sink + 16 * lane;
+    const int64_t spitch = st ? a.pitch : 0;
+    const int64_t n = a.r1 - ys < R ? a.r1 - ys : R;
+    if (n == R)
+        strip_full<E, R, D, WRAPX>(c, ys, dst, spitch);
+    else
+        strip_tail<E, WRAPX>(c, ys, (int)n, dst, spitch);
+}
+
+// ------------------------------------------------------------------ cell access
+// Byte: cell x of a padded row at row[xoff + x].  Bit: word (x >> 5) (floor)
+// of the dword array starting at row + xoff, bit (x & 31).
+__device__ __forceinline__ uint32_t get_cell(const uint8_t *row, int64_t xoff, int64_t x, bool bit) {
+    if (!bit) return row[xoff + x];
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(row + xoff);
+    return (w[x >> 5] >> (x & 31)) & 1u;
+}
+__device__ __forceinline__ void set_cell(uint8_t *row, int64_t xoff, int64_t x, uint32_t v, bool bit) {
+    if (!bit) {
+        row[xoff + x] = (uint8_t)v;
+        return;
+    }
+    uint32_t *w = reinterpret_cast<uint32_t *>(row + xoff);
+    const uint32_t m = 1u << (x & 31);
+    w[x >> 5] = (w[x >> 5] & ~m) | (v ? m : 0u);
+}
+
+__global__ void pack_columns_kernel(const uint8_t *buf, int64_t pitch, int64_t xoff, int64_t w, int64_t h,
+                                    uint8_t *stage, bool bit) {
+    const int64_t y = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (y >= h) return;
+    const uint8_t *row = buf + (y + 1) * pitch;
+    stage[y] = (uint8_t)get_cell(row, xoff, w - 1, bit);
+    stage[h + y] = (uint8_t)get_cell(row, xoff, 0, bit);
+}
+
+__global__ void unpack_columns_kernel(uint8_t *buf, int64_t pitch, int64_t xoff, int64_t w, int64_t h,
+                                      const uint8_t *stage, bool bit) {
+    const int64_t y = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (y >= h) return;
+    uint8_t *row = buf + (y + 1) * pitch;
+    set_cell(row, xoff, -1, stage[y] ? 1u : 0u, bit);
+    set_cell(row, xoff, w, stage[h + y] ? 1u : 0u, bit);
+}
+
+// One thread per 16-byte unit of an owned row: dense (row pitch w) -> padded.
+template <int CPU>  // cells per unit: 16 (byte) or 128 (bit)
+__global__ void import_kernel(const uint8_t *dense, uint8_t *buf, int64_t pitch, int64_t xoff, int64_t w,
+                              int64_t h, int64_t units) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= units * h) return;
+    const int64_t u = i % units, y = i / units;
+    const uint8_t *in = dense + y * w;
+    uint32_t word[4] = {0u, 0u, 0u, 0u};
+    const int64_t x0 = u * CPU;
+    for (int k = 0; k < CPU; ++k) {
+        const int64_t x = x0 + k;
+        if (x >= w) break;
+        const uint32_t v = in[x] != 0;
+        if (CPU == 16)
+            word[k >> 2] |= v << (8 * (k & 3));
+        else
+            word[k >> 5] |= v << (k & 31);
+    }
+    *reinterpret_cast<uint4 *>(buf + (y + 1) * pitch + xoff + 16 * u) =
+        make_uint4(word[0], word[1], word[2], word[3]);
+}
+
+template <int CPU>
+__global__ void export_kernel(const uint8_t *buf, uint8_t *dense, int64_t pitch, int64_t xoff, int64_t w,
+                              int64_t h, int64_t units) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= units * h) return;
+    const int64_t u = i % units, y = i / units;
+    const uint4 q = *reinterpret_cast<const uint4 *>(buf + (y + 1) * pitch + xoff + 16 * u);
+    const uint32_t word[4] = {q.x, q.y, q.z, q.w};
+    uint8_t *o = dense + y * w;
+    const int64_t x0 = u * CPU;
+    for (int k = 0; k < CPU; ++k) {
+        const int64_t x = x0 + k;
+        if (x >= w) break;
+        o[x] = CPU == 16 ? (uint8_t)((word[k >> 2] >> (8 * (k & 3))) & 0xFFu)
+                         : (uint8_t)((word[k >> 5] >> (k & 31)) & 1u);
+    }
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+template <int CPU>
+__global__ void fill_random_kernel(uint8_t *buf, int64_t pitch, int64_t xoff, int64_t w, int64_t h,
+                                   int64_t units, int64_t gx0, int64_t gy0, int64_t nx, uint64_t key,
+                                   uint32_t thr) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= units * h) return;
+    const int64_t u = i % units, y = i / units;
+    uint32_t word[4] = {0u, 0u, 0u, 0u};
+    const int64_t x0 = u * CPU;
+    const uint64_t base = (uint64_t)((gy0 + y) * nx + gx0);
+    for (int k = 0; k < CPU; ++k) {
+        const int64_t x = x0 + k;
+        if (x >= w) break;
+        const uint32_t v = (uint32_t)(splitmix64(key ^ (base + (uint64_t)x)) >> 32) < thr;
+        if (CPU == 16)
+            word[k >> 2] |= v << (8 * (k & 3));
+        else
+            word[k >> 5] |= v << (k & 31);
+    }
+    *reinterpret_cast<uint4 *>(buf + (y + 1) * pitch + xoff + 16 * u) =
+        make_uint4(word[0], word[1], word[2], word[3]);
+}
+
+template <int CPU>
+__global__ void live_count_kernel(const uint8_t *buf, int64_t pitch, int64_t xoff, int64_t w, int64_t h,
+                                  int64_t units, unsigned long long *count) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long c = 0;
+    if (i < units * h) {
+        const int64_t u = i % units, y = i / units;
+        const uint4 q = *reinterpret_cast<const uint4 *>(buf + (y + 1) * pitch + xoff + 16 * u);
+        const uint32_t word[4] = {q.x, q.y, q.z, q.w};
+        const int64_t valid = w - u * CPU;  // cells of this unit inside the block
+        constexpr int kPerWord = CPU / 4;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t left = valid - k * kPerWord;
+            uint32_t m;
+            if (left <= 0)
+                m = 0u;
+            else if (left >= kPerWord)
+                m = 0xFFFFFFFFu;
+            else
+                m = CPU == 16 ? (0xFFFFFFFFu >> (32 - 8 * left)) : (0xFFFFFFFFu >> (32 - left));
+            c += __popc(word[k] & m);  // byte cells are 0/1: popcount == sum
+        }
+    }
+    for (int s = 32; s > 0; s >>= 1) c += __shfl_xor(c, s);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(count, c);
+}
+
+inline bool is_bit(const life_layout &L) { return L.kernel == LIFE_KERNEL_BIT; }
+inline unsigned blocks_for(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
+
+}  // namespace
+
+namespace {
+// Measured on MI355X at 65536^2 (scripts/tune.py, profiles/): bit R16/D8 and
+// byte R64/D2 were the fastest of {16,32,64} x {2,4,8}.
+struct Tunings {
+    StepTuning t[2];  // [0] byte, [1] bit
+    Tunings() : t{{64, 2}, {16, 8}} {
+        for (StepTuning &v : t) {
+            if (const char *e = getenv("LIFE_STEP_ROWS")) v.rows = atoi(e);
+            if (const char *e = getenv("LIFE_STEP_DEPTH")) v.depth = atoi(e);
+        }
+    }
+};
+Tunings &tunings() {
+    static Tunings t;
+    return t;
+}
+}  // namespace
+
+StepTuning step_tuning(bool bit) { return tunings().t[bit ? 1 : 0]; }
+
+void set_step_tuning(int kernel, int rows, int depth) {
+    for (int k = 0; k < 2; k++) {
+        if (kernel >= 0 && kernel != k) continue;
+        if (rows == 16 || rows == 32 || rows == 64) tunings().t[k].rows = rows;
+        if (depth == 2 || depth == 4 || depth == 8) tunings().t[k].depth = depth;
+    }
+}
+
+namespace {
+template <class E, int R, int D>
+hipError_t launch_rd(const StepArgs &a, bool wrapx, unsigned grid, hipStream_t s) {
+    if (wrapx)
+        step_kernel<E, R, D, true><<<grid, kBlock, 0, s>>>(a);
+    else
+        step_kernel<E, R, D, false><<<grid, kBlock, 0, s>>>(a);
+    return hipGetLastError();
+}
+
+template <class E, int R>
+hipError_t launch_r(const StepArgs &a, int depth, bool wrapx, unsigned grid, hipStream_t s) {
+    switch (depth) {
+    case 2: return launch_rd<E, R, 2>(a, wrapx, grid, s);
+    case 8: return launch_rd<E, R, 8>(a, wrapx, grid, s);
+    default: return launch_rd<E, R, 4>(a, wrapx, grid, s);
+    }
+}
+
+template <class E>
+hipError_t launch_e(const StepArgs &a, const StepTuning &t, bool wrapx, unsigned grid, hipStream_t s) {
+    switch (t.rows) {
+    case 16: return launch_r<E, 16>(a, t.depth, wrapx, grid, s);
+    case 64: return launch_r<E, 64>(a, t.depth, wrapx, grid, s);
+    default: return launch_r<E, 32>(a, t.depth, wrapx, grid, s);
+    }
+}
+}  // namespace
+
+hipError_t launch_step(const life_layout &L, const uint8_t *in, uint8_t *out, uint8_t *sink,
+                       const Region &reg, Wrap wrap, hipStream_t s) {
+    if (reg.u1 <= reg.u0 || reg.r1 <= reg.r0) return hipSuccess;
+    StepTuning t = step_tuning(is_bit(L));
+    if (t.rows != 16 && t.rows != 64) t.rows = 32;
+    StepArgs a;
+    a.in = in;
+    a.out = out;
+    a.sink = sink;
+    a.pitch = L.pitch;
+    a.xoff = L.xoff;
+    a.units = L.units;
+    a.w = L.w;
+    a.h = L.h;
+    a.u0 = reg.u0;
+    a.u1 = reg.u1;
+    a.r0 = reg.r0;
+    a.r1 = reg.r1;
+    a.nbx = (reg.u1 - reg.u0 + kBlock - 1) / kBlock;
+    a.wrapy = wrap.y ? 1 : 0;
+    const int64_t nby = (reg.r1 - reg.r0 + t.rows - 1) / t.rows;
+    const unsigned grid = (unsigned)(a.nbx * nby);
+    return is_bit(L) ? launch_e<BitEnc>(a, t, wrap.x, grid, s) : launch_e<ByteEnc>(a, t, wrap.x, grid, s);
+}
+
+hipError_t launch_pack_columns(const life_layout &L, const uint8_t *buf, uint8_t *stage, hipStream_t s) {
+    pack_columns_kernel<<<blocks_for(L.h, 256), 256, 0, s>>>(buf, L.pitch, L.xoff, L.w, L.h, stage, is_bit(L));
+    return hipGetLastError();
+}
+
+hipError_t launch_unpack_columns(const life_layout &L, uint8_t *buf, const uint8_t *stage, hipStream_t s) {
+    unpack_columns_kernel<<<blocks_for(L.h, 256), 256, 0, s>>>(buf, L.pitch, L.xoff, L.w, L.h, stage,
+                                                                is_bit(L));
+    return hipGetLastError();
+}
+
+hipError_t launch_import_block(const life_layout &L, const uint8_t *dense, uint8_t *buf, hipStream_t s) {
+    const unsigned g = blocks_for(L.units * L.h, 256);
+    if (is_bit(L))
+        import_kernel<128><<<g, 256, 0, s>>>(dense, buf, L.pitch, L.xoff, L.w, L.h, L.units);
+    else
+        import_kernel<16><<<g, 256, 0, s>>>(dense, buf, L.pitch, L.xoff, L.w, L.h, L.units);
+    return hipGetLastError();
+}
+
+hipError_t launch_export_block(const life_layout &L, const uint8_t *buf, uint8_t *dense, hipStream_t s) {
+    const unsigned g = blocks_for(L.units * L.h, 256);
+    if (is_bit(L))
+        export_kernel<128><<<g, 256, 0, s>>>(buf, dense, L.pitch, L.xoff, L.w, L.h, L.units);
+    else
+        export_kernel<16><<<g, 256, 0, s>>>(buf, dense, L.pitch, L.xoff, L.w, L.h, L.units);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill_random(const life_layout &L, int64_t nx, uint64_t key, uint32_t thr32, uint8_t *buf,
+                              hipStream_t s) {
+    const unsigned g = blocks_for(L.units * L.h, 256);
+    if (is_bit(L))
+        fill_random_kernel<128><<<g, 256, 0, s>>>(buf, L.pitch, L.xoff, L.w, L.h, L.units, L.x0, L.y0, nx,
+                                                  key, thr32);
+    else
+        fill_random_kernel<16><<<g, 256, 0, s>>>(buf, L.pitch, L.xoff, L.w, L.h, L.units, L.x0, L.y0, nx,
+                                                 key, thr32);
+    return hipGetLastError();
+}
+
+hipError_t launch_live_count(const life_layout &L, const uint8_t *buf, unsigned long long *count,
+                             hipStream_t s) {
+    const unsigned g = blocks_for(L.units * L.h, 256);
+    if (is_bit(L))
+        live_count_kernel<128><<<g, 256, 0, s>>>(buf, L.pitch, L.xoff, L.w, L.h, L.units, count);
+    else
+        live_count_kernel<16><<<g, 256, 0, s>>>(buf, L.pitch, L.xoff, L.w, L.h, L.units, count);
+    return hipGetLastError();
+}
+
+}  // namespace life

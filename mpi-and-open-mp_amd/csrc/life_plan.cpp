@@ -1,0 +1,129 @@
+// life_plan.cpp -- host-only partition, layout and halo plan (no HIP calls,
+// callable without a GPU).
+//
+// Replaces the reference's MPI Cartesian set-up and exchange schedule:
+//   MPI_Dims_create / MPI_Cart_create / MPI_Cart_coords  life_cart.c:117-121
+//   decomposition()                                      life_cart.c:217-223
+//   exchange_columns / exchange_rows / exchange_corners  life_cart.c:225-279
+// The corner messages are dropped: columns go first, then rows of width+2
+// carry the freshly received column apron (the corners) along.
+#include <stdio.h>
+#include <string.h>
+
+#include "life_mi355x.h"
+
+namespace {
+constexpr int64_t kXoff = 128;  // owned x = 0 starts 128 B into a padded row
+inline int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+inline int cart_rank(int c0, int c1, int dims1) { return c0 * dims1 + c1; }
+}  // namespace
+
+extern "C" {
+
+void life_decomposition(int64_t n, int p, int k, int64_t *start, int64_t *stop) {
+    const int64_t l = n / p;  // life_cart.c:218
+    *start = l * k;
+    *stop = *start + l;
+    if (k == p - 1) *stop = n;  // the last block takes the remainder (:221-222)
+}
+
+void life_dims_create(int n, int dims[2]) {
+    // MPI_Dims_create(n, 2, {0,0}): most balanced factor pair, non-increasing.
+    int d1 = 1;
+    for (int f = 1; (int64_t)f * f <= n; f++)
+        if (n % f == 0) d1 = f;
+    dims[0] = n / d1;
+    dims[1] = d1;
+}
+
+int life_layout_query(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int kernel,
+                      life_layout *out) {
+    if (!out || nx <= 0 || ny <= 0 || dims0 <= 0 || dims1 <= 0 || rank < 0 ||
+        rank >= dims0 * dims1 || (kernel != LIFE_KERNEL_BYTE && kernel != LIFE_KERNEL_BIT))
+        return LIFE_EINVAL;
+    if (nx < dims0 || ny < dims1) return LIFE_EINVAL;  // no empty blocks
+    memset(out, 0, sizeof *out);
+    const int c0 = rank / dims1, c1 = rank % dims1;  // MPI_Cart_coords, row-major
+    int64_t xs, xe, ys, ye;
+    life_decomposition(nx, dims0, c0, &xs, &xe);
+    life_decomposition(ny, dims1, c1, &ys, &ye);
+    out->w = xe - xs;
+    out->h = ye - ys;
+    out->x0 = xs;
+    out->y0 = ys;
+    out->kernel = kernel;
+    out->coords[0] = c0;
+    out->coords[1] = c1;
+    const int64_t cells_per_unit = kernel == LIFE_KERNEL_BIT ? 128 : 16;
+    out->units = (out->w + cells_per_unit - 1) / cells_per_unit;
+    out->xoff = kXoff;
+    // room for the last unit, the right-apron cell and the right extra dword
+    out->pitch = round_up(kXoff + 16 * out->units + 16, 256);
+    out->rows = out->h + 2;
+    return LIFE_OK;
+}
+
+int life_halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, life_halo_op *ops,
+                   int max_ops) {
+    life_layout L;
+    const int rc = life_layout_query(nx, ny, dims0, dims1, rank, LIFE_KERNEL_BYTE, &L);
+    if (rc != LIFE_OK) return rc;
+    const int c0 = L.coords[0], c1 = L.coords[1];
+    const int64_t w = L.w, h = L.h;
+    life_halo_op tmp[10];
+    int n = 0;
+    auto add = [&](int phase, int kind, int peer, int what, int64_t index, int64_t first, int64_t count) {
+        life_halo_op &o = tmp[n++];
+        o.phase = phase;
+        o.kind = kind;
+        o.peer = peer;
+        o.what = what;
+        o.index = index;
+        o.first = first;
+        o.count = count;
+    };
+    // Phase 0: columns (dim 0 splits x).  MPI_Cart_shift(dim 0): left/right.
+    if (dims0 == 1) {
+        add(0, LIFE_HALO_FILL, -1, LIFE_HALO_COLUMN, -1, 1, h);
+    } else {
+        const int right = cart_rank((c0 + 1) % dims0, c1, dims1);
+        const int left = cart_rank((c0 - 1 + dims0) % dims0, c1, dims1);
+        // life_cart.c:251-254 order: Send right, Recv left, Send left, Recv right.
+        add(0, LIFE_HALO_SEND, right, LIFE_HALO_COLUMN, w - 1, 1, h);
+        add(0, LIFE_HALO_SEND, left, LIFE_HALO_COLUMN, 0, 1, h);
+        add(0, LIFE_HALO_RECV, left, LIFE_HALO_COLUMN, -1, 1, h);
+        add(0, LIFE_HALO_RECV, right, LIFE_HALO_COLUMN, w, 1, h);
+    }
+    // Phase 1: rows of width+2 (x = -1 .. w), carrying the corners.
+    if (dims1 == 1) {
+        add(1, LIFE_HALO_FILL, -1, LIFE_HALO_ROW, 0, -1, w + 2);
+    } else {
+        const int right = cart_rank(c0, (c1 + 1) % dims1, dims1);
+        const int left = cart_rank(c0, (c1 - 1 + dims1) % dims1, dims1);
+        // life_cart.c:235-238 order.
+        add(1, LIFE_HALO_SEND, right, LIFE_HALO_ROW, h, -1, w + 2);
+        add(1, LIFE_HALO_SEND, left, LIFE_HALO_ROW, 1, -1, w + 2);
+        add(1, LIFE_HALO_RECV, left, LIFE_HALO_ROW, 0, -1, w + 2);
+        add(1, LIFE_HALO_RECV, right, LIFE_HALO_ROW, h + 1, -1, w + 2);
+    }
+    if (ops) {
+        if (max_ops < n) return LIFE_EINVAL;
+        memcpy(ops, tmp, sizeof(life_halo_op) * n);
+    }
+    return n;
+}
+
+const char *life_strerror(int err) {
+    switch (err) {
+    case LIFE_OK: return "success";
+    case LIFE_EINVAL: return "invalid argument";
+    case LIFE_EHIP: return "HIP runtime error";
+    case LIFE_ERCCL: return "RCCL error";
+    case LIFE_ENOMEM: return "out of memory";
+    case LIFE_ESTATE: return "invalid state";
+    case LIFE_EIO: return "I/O or parse error";
+    default: return "unknown error";
+    }
+}
+
+}  // extern "C"

@@ -1,0 +1,263 @@
+"""life_mi355x -- Python binding of the MI355X Game-of-Life C ABI.
+
+Mirrors the reference's per-rank interface (6-cartesian/life_cart.c:39-49):
+
+=====================  ==============================================
+reference              here
+=====================  ==============================================
+life_init (loader)     :func:`load_cfg` (cfg.py) + :class:`Life`
+life_step              :meth:`Life.step`  (HIP kernels)
+life_exchange          part of :meth:`Life.step` (RCCL / local halo)
+life_collect           :meth:`Life.gather` (device-side gather)
+life_save_vtk          :func:`save_vtk` (cfg.py)
+decomposition          :func:`decomposition`
+MPI_Dims_create        :func:`dims_create`
+life_free              :meth:`Life.close`
+=====================  ==============================================
+
+The compute path is ``liblife_mi355x.so`` only: there is no CPU fallback.
+Importing works without a GPU (host-only helpers such as
+:func:`halo_plan` run anywhere); device calls raise :class:`LifeError` when
+no HIP device is present.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from .cfg import load_cfg, save_vtk, vtk_bytes  # noqa: F401
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liblife_mi355x.so")
+
+KERNEL_BYTE = 0
+KERNEL_BIT = 1
+KERNELS = {"byte": KERNEL_BYTE, "bit": KERNEL_BIT}
+XPORT_AUTO, XPORT_RCCL, XPORT_LOCAL = 0, 1, 2
+HALO_SEND, HALO_RECV, HALO_FILL = 0, 1, 2
+HALO_COLUMN, HALO_ROW = 0, 1
+
+# Every symbol include/life_mi355x.h declares (checked by tests/test_abi.py).
+ABI_SYMBOLS = (
+    "life_decomposition", "life_dims_create", "life_halo_plan", "life_layout_query",
+    "life_strerror", "life_last_error", "life_dev_create", "life_dev_create_ex",
+    "life_get_unique_id", "life_dev_create_rank", "life_dev_upload", "life_dev_fill_random",
+    "life_dev_step", "life_dev_gather", "life_dev_live_count", "life_dev_sync",
+    "life_dev_layout", "life_dev_world", "life_dev_set_timing", "life_dev_kernel_stats",
+    "life_tune", "life_dev_destroy",
+)
+
+
+class LifeError(RuntimeError):
+    def __init__(self, rc: int, what: str):
+        lib = _lib()
+        detail = lib.life_last_error().decode(errors="replace")
+        super().__init__(f"{what}: {lib.life_strerror(rc).decode()} ({rc}){': ' + detail if detail else ''}")
+        self.rc = rc
+
+
+class HaloOp(ctypes.Structure):
+    _fields_ = [("phase", ctypes.c_int32), ("kind", ctypes.c_int32), ("peer", ctypes.c_int32),
+                ("what", ctypes.c_int32), ("index", ctypes.c_int64), ("first", ctypes.c_int64),
+                ("count", ctypes.c_int64)]
+
+    def as_tuple(self):
+        return (self.phase, self.kind, self.peer, self.what, self.index, self.first, self.count)
+
+
+class Layout(ctypes.Structure):
+    _fields_ = [("w", ctypes.c_int64), ("h", ctypes.c_int64), ("x0", ctypes.c_int64),
+                ("y0", ctypes.c_int64), ("pitch", ctypes.c_int64), ("xoff", ctypes.c_int64),
+                ("rows", ctypes.c_int64), ("units", ctypes.c_int64), ("kernel", ctypes.c_int32),
+                ("coords", ctypes.c_int32 * 2)]
+
+
+_LIB = None
+
+
+def _lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is not built: run `make -C mpi-and-open-mp_amd` "
+                              "or __graft_entry__.build()")
+        L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        i64, i32, vp = ctypes.c_int64, ctypes.c_int, ctypes.c_void_p
+        P = ctypes.POINTER
+        L.life_decomposition.argtypes = [i64, i32, i32, P(i64), P(i64)]
+        L.life_decomposition.restype = None
+        L.life_dims_create.argtypes = [i32, P(ctypes.c_int)]
+        L.life_dims_create.restype = None
+        L.life_halo_plan.argtypes = [i64, i64, i32, i32, i32, P(HaloOp), i32]
+        L.life_layout_query.argtypes = [i64, i64, i32, i32, i32, i32, P(Layout)]
+        L.life_strerror.argtypes = [i32]
+        L.life_strerror.restype = ctypes.c_char_p
+        L.life_last_error.restype = ctypes.c_char_p
+        L.life_dev_create.argtypes = [i64, i64, i32, i32, P(vp)]
+        L.life_dev_create_ex.argtypes = [i64, i64, i32, i32, i32, i32, i32, P(vp)]
+        L.life_get_unique_id.argtypes = [ctypes.c_char_p]
+        L.life_dev_create_rank.argtypes = [i64, i64, i32, i32, i32, i32, i32, ctypes.c_char_p, i32, P(vp)]
+        L.life_dev_upload.argtypes = [vp, P(ctypes.c_uint8)]
+        L.life_dev_fill_random.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint32]
+        L.life_dev_step.argtypes = [vp, i64]
+        L.life_dev_gather.argtypes = [vp, P(ctypes.c_uint8)]
+        L.life_dev_live_count.argtypes = [vp]
+        L.life_dev_live_count.restype = i64
+        L.life_dev_sync.argtypes = [vp]
+        L.life_dev_layout.argtypes = [vp, i32, P(Layout)]
+        L.life_dev_world.argtypes = [vp] + [P(ctypes.c_int)] * 5
+        L.life_dev_set_timing.argtypes = [vp, i32]
+        L.life_dev_kernel_stats.argtypes = [vp, P(ctypes.c_double), P(i64), P(ctypes.c_double)]
+        L.life_tune.argtypes = [i32, i32, i32]
+        L.life_dev_destroy.argtypes = [vp]
+        L.life_dev_destroy.restype = None
+        _LIB = L
+    return _LIB
+
+
+def _check(rc: int, what: str) -> int:
+    if rc < 0:
+        raise LifeError(rc, what)
+    return rc
+
+
+def kernel_id(kernel) -> int:
+    if isinstance(kernel, str):
+        return KERNELS[kernel]
+    return int(kernel)
+
+
+# ---------------------------------------------------------------- host only
+def decomposition(n: int, p: int, k: int):
+    """life_cart.c:217-223 -> (start, stop)."""
+    s, e = ctypes.c_int64(), ctypes.c_int64()
+    _lib().life_decomposition(n, p, k, ctypes.byref(s), ctypes.byref(e))
+    return s.value, e.value
+
+
+def dims_create(n: int):
+    """MPI_Dims_create(n, 2, {0,0}) (life_cart.c:117-118)."""
+    d = (ctypes.c_int * 2)()
+    _lib().life_dims_create(n, d)
+    return d[0], d[1]
+
+
+def halo_plan(nx: int, ny: int, dims, rank: int):
+    """The per-generation halo ops of shard `rank` (see life_halo_plan)."""
+    ops = (HaloOp * 16)()
+    n = _check(_lib().life_halo_plan(nx, ny, dims[0], dims[1], rank, ops, 16), "life_halo_plan")
+    return [ops[i].as_tuple() for i in range(n)]
+
+
+def layout_query(nx: int, ny: int, dims, rank: int, kernel="byte") -> Layout:
+    L = Layout()
+    _check(_lib().life_layout_query(nx, ny, dims[0], dims[1], rank, kernel_id(kernel), ctypes.byref(L)),
+           "life_layout_query")
+    return L
+
+
+def density_to_thr(density: float) -> int:
+    return min(int(density * 2.0**32), 0xFFFFFFFF)
+
+
+def tune(rows: int = 0, depth: int = 0, kernel=-1) -> None:
+    """Stencil rows-per-lane / prefetch depth for this process (life_tune)."""
+    _check(_lib().life_tune(kernel_id(kernel), rows, depth), "life_tune")
+
+
+def unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(128)
+    _check(_lib().life_get_unique_id(buf), "life_get_unique_id")
+    return buf.raw
+
+
+# ---------------------------------------------------------------- device
+class Life:
+    """A periodic nx x ny Game of Life resident in MI355X HBM.
+
+    ``Life(nx, ny, shards=1, kernel="bit")`` drives ``shards`` Cartesian
+    blocks from this process (one per GPU, or several logical shards on one
+    GPU with the LOCAL transport).  :meth:`for_rank` is the
+    one-process-per-GPU form (torchrun), with RCCL between ranks.
+    """
+
+    def __init__(self, nx: int, ny: int, shards: int = 1, kernel="bit", dims=(0, 0),
+                 transport: int = XPORT_AUTO, _handle=None):
+        self.nx, self.ny = int(nx), int(ny)
+        self.kernel = kernel_id(kernel)
+        self._h = ctypes.c_void_p()
+        if _handle is not None:
+            self._h = _handle
+        else:
+            _check(_lib().life_dev_create_ex(self.nx, self.ny, shards, dims[0], dims[1], self.kernel,
+                                             transport, ctypes.byref(self._h)), "life_dev_create")
+
+    @classmethod
+    def for_rank(cls, nx, ny, rank, world, uid: bytes, device: int, kernel="bit", dims=(0, 0)):
+        h = ctypes.c_void_p()
+        _check(_lib().life_dev_create_rank(nx, ny, kernel_id(kernel), rank, world, dims[0], dims[1],
+                                           uid, device, ctypes.byref(h)), "life_dev_create_rank")
+        return cls(nx, ny, kernel=kernel, _handle=h)
+
+    # life_init's cell loading (life_cart.c:104-109)
+    def upload(self, grid: np.ndarray) -> None:
+        g = np.ascontiguousarray(grid, dtype=np.uint8)
+        if g.shape != (self.ny, self.nx):
+            raise ValueError(f"grid shape {g.shape} != ({self.ny}, {self.nx})")
+        _check(_lib().life_dev_upload(self._h, g.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))), "upload")
+
+    def fill_random(self, seed: int, density: float = 0.5) -> None:
+        _check(_lib().life_dev_fill_random(self._h, seed, density_to_thr(density)), "fill_random")
+
+    def step(self, generations: int = 1) -> None:
+        _check(_lib().life_dev_step(self._h, generations), "step")
+
+    def gather(self, out: np.ndarray | None = None) -> np.ndarray:
+        if out is None:
+            out = np.empty((self.ny, self.nx), dtype=np.uint8)
+        _check(_lib().life_dev_gather(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))), "gather")
+        return out
+
+    def live_count(self) -> int:
+        return _check(_lib().life_dev_live_count(self._h), "live_count")
+
+    def sync(self) -> None:
+        _check(_lib().life_dev_sync(self._h), "sync")
+
+    def layout(self, local_shard: int = 0) -> Layout:
+        L = Layout()
+        _check(_lib().life_dev_layout(self._h, local_shard, ctypes.byref(L)), "layout")
+        return L
+
+    def world(self):
+        v = [ctypes.c_int() for _ in range(5)]
+        _check(_lib().life_dev_world(self._h, *[ctypes.byref(x) for x in v]), "world")
+        return dict(zip(("world", "dims0", "dims1", "nlocal", "transport"), (x.value for x in v)))
+
+    def set_timing(self, on: bool) -> None:
+        _check(_lib().life_dev_set_timing(self._h, int(on)), "set_timing")
+
+    def kernel_stats(self):
+        ms, n, b = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+        _check(_lib().life_dev_kernel_stats(self._h, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(b)),
+               "kernel_stats")
+        return ms.value, n.value, b.value
+
+    def close(self) -> None:
+        if self._h:
+            _lib().life_dev_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""A/B the stencil variants (rows per lane x prefetch depth) in ONE process,
+interleaved over rounds, at the bench workload (random 50% N^2, 1 GPU).
+
+Prints one JSON line per (kernel, rows, depth): median / min kernel ms and
+the algorithmic GB/s, plus the live count after the run (every variant must
+agree: they compute the same generations).
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "mpi-and-open-mp_amd"))
+import life_mi355x as lm  # noqa: E402
+
+p = argparse.ArgumentParser()
+p.add_argument("--size", type=int, default=65536)
+p.add_argument("--kernels", default="bit,byte")
+p.add_argument("--rows", default="16,32,64")
+p.add_argument("--depths", default="2,4,8")
+p.add_argument("--gens", type=int, default=10)
+p.add_argument("--rounds", type=int, default=3)
+a = p.parse_args()
+
+variants = [(r, d) for r in map(int, a.rows.split(",")) for d in map(int, a.depths.split(","))]
+for kernel in a.kernels.split(","):
+    life = lm.Life(a.size, a.size, kernel=kernel)
+    life.fill_random(1, 0.5)
+    res = {v: [] for v in variants}
+    lives = {}
+    for rnd in range(a.rounds):
+        for v in variants:
+            lm.tune(*v, kernel=kernel)
+            life.step(2)  # warm
+            life.sync()
+            life.set_timing(True)
+            life.step(a.gens)
+            ms, n, b = life.kernel_stats()
+            life.set_timing(False)
+            res[v].append((ms, b))
+            lives[v] = life.live_count()
+    for v in variants:
+        mss = [m for m, _ in res[v]]
+        b = res[v][0][1]
+        med = statistics.median(mss)
+        print(json.dumps({"kernel": kernel, "rows": v[0], "depth": v[1], "median_ms": round(med, 4),
+                          "min_ms": round(min(mss), 4), "GBps_median": round(b / med / 1e6, 1),
+                          "GBps_best": round(b / min(mss) / 1e6, 1), "live": lives[v]}), flush=True)
+    life.close()
