@@ -28,7 +28,13 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "mpi-and-open-mp_amd"))
 
-import life_mi355x as lm  # noqa: E402  (loads liblife_mi355x.so before torch)
+if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    # torch bundles its own HIP runtime and links it by its unversioned name;
+    # loading torch FIRST makes liblife_mi355x.so bind to that same runtime
+    # (SONAME libamdhip64.so.7) instead of a second copy from /opt/rocm.
+    import torch.distributed  # noqa: F401
+
+import life_mi355x as lm  # noqa: E402
 
 lm._lib()
 

@@ -1,0 +1,132 @@
+"""Host-side logic of the product (no GPU): .cfg loader, VTK writer,
+decomposition / dims, layout and the halo plan."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+with open(os.path.join(GOLDEN, "golden.json")) as _f:
+    G = json.load(_f)
+
+
+def test_cfg_loader_matches_reference_frame0(lm):
+    for name, rec in G["patterns"].items():
+        steps, save, grid = lm.load_cfg(os.path.join(GOLDEN, "cfg", name + ".cfg"))
+        assert hashlib.md5(lm.vtk_bytes(grid)).hexdigest() == rec["frames"]["0"][0]
+
+
+def test_cfg_loader_wraps_and_dedups(lm, tmp_path):
+    p = tmp_path / "w.cfg"
+    p.write_text("3\n1\n4 3\n0 0\n0 0\n-1 -1\n4 3\n-5 7\n")
+    steps, save, g = lm.load_cfg(str(p))
+    assert (steps, save, g.shape) == (3, 1, (3, 4))
+    want = np.zeros((3, 4), np.uint8)
+    want[0, 0] = want[2, 3] = want[1, 3] = 1  # (-1,-1)->(3,2); (4,3)->(0,0); (-5,7)->(3,1)
+    np.testing.assert_array_equal(g, want)
+
+
+def test_cfg_loader_rejects_malformed(lm, tmp_path):
+    p = tmp_path / "bad.cfg"
+    p.write_text("3\n1\n4 3\n0\n")
+    with pytest.raises(ValueError):
+        lm.load_cfg(str(p))
+
+
+@pytest.mark.reference
+def test_cfg_loader_vs_reference_loader(lm, oracle):
+    import ctypes
+
+    ref = oracle.ref_lib()
+    if ref is None:
+        pytest.skip("oracle/_ref not built")
+    for name in G["patterns"]:
+        path = os.path.join(GOLDEN, "cfg", name + ".cfg").encode()
+        v = [ctypes.c_int() for _ in range(4)]
+        ref.ref_load_cfg(path, *[ctypes.byref(x) for x in v], None)
+        grid = np.zeros((v[3].value, v[2].value), np.uint8)
+        ref.ref_load_cfg(path, *[ctypes.byref(x) for x in v], grid.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+        steps, save, mine = lm.load_cfg(path.decode())
+        assert (steps, save) == (v[0].value, v[1].value)
+        np.testing.assert_array_equal(mine, grid)
+
+
+@pytest.mark.reference
+def test_vtk_writer_vs_reference_writer(lm, oracle, tmp_path):
+    import ctypes
+
+    ref = oracle.ref_lib()
+    if ref is None:
+        pytest.skip("oracle/_ref not built")
+    g = oracle.fill_random(37, 11, 3, 0.5)
+    path = str(tmp_path / "ref.vtk").encode()
+    ref.ref_save_vtk(path, 37, 11, g.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+    assert open(path, "rb").read() == lm.vtk_bytes(g)
+
+
+@pytest.mark.parametrize("n,p", [(10, 3), (500, 4), (7, 7), (65536, 4), (1 << 40, 8)])
+def test_decomposition(lm, oracle, n, p):
+    blocks = [lm.decomposition(n, p, k) for k in range(p)]
+    assert blocks == [oracle.decomposition(n, p, k) for k in range(p)]
+    assert blocks[0][0] == 0 and blocks[-1][1] == n
+    assert all(blocks[k][1] == blocks[k + 1][0] for k in range(p - 1))
+
+
+def test_dims_create_matches_mpi(lm):
+    # MPI_Dims_create(n, 2) values measured under MPICH plus
+    # the balanced-factor rule for others.
+    want = {1: (1, 1), 2: (2, 1), 3: (3, 1), 4: (2, 2), 5: (5, 1), 6: (3, 2), 8: (4, 2), 12: (4, 3), 16: (4, 4)}
+    for n, d in want.items():
+        assert lm.dims_create(n) == d
+
+
+@pytest.mark.parametrize("kernel", ["byte", "bit"])
+@pytest.mark.parametrize("nx,ny,dims", [(1, 1, (1, 1)), (65536, 65536, (1, 1)), (1000, 37, (4, 2)),
+                                        (3, 2, (3, 2)), (262144, 131072, (4, 2))])
+def test_layout_invariants(lm, kernel, nx, ny, dims):
+    for r in range(dims[0] * dims[1]):
+        L = lm.layout_query(nx, ny, dims, r, kernel)
+        cpu = 128 if kernel == "bit" else 16
+        assert L.units == -(-L.w // cpu)
+        assert L.pitch % 256 == 0 and L.xoff % 16 == 0
+        assert L.pitch >= L.xoff + 16 * L.units + 16  # last unit, apron cell, right extra dword
+        assert L.rows == L.h + 2
+        assert (L.x0, L.x0 + L.w) == lm.decomposition(nx, dims[0], r // dims[1])
+        assert (L.y0, L.y0 + L.h) == lm.decomposition(ny, dims[1], r % dims[1])
+
+
+def test_layout_rejects_empty_blocks(lm):
+    with pytest.raises(lm.LifeError):
+        lm.layout_query(3, 10, (4, 1), 0)
+
+
+@pytest.mark.parametrize("nx,ny,dims", [(10, 10, (2, 2)), (500, 500, (4, 2)), (7, 5, (2, 1)), (7, 5, (1, 2)),
+                                        (9, 9, (3, 3)), (5, 5, (1, 1)), (100, 3, (4, 3))])
+def test_halo_plan_is_symmetric(lm, nx, ny, dims):
+    """Every recv has a matching send at the peer: same phase, same size,
+    matched in issue order (RCCL p2p semantics), and sends go to the Cartesian
+    neighbour whose apron they fill."""
+    world = dims[0] * dims[1]
+    plans = {r: lm.halo_plan(nx, ny, dims, r) for r in range(world)}
+    lay = {r: lm.layout_query(nx, ny, dims, r) for r in range(world)}
+    for r, ops in plans.items():
+        for phase in (0, 1):
+            ph = [o for o in ops if o[0] == phase]
+            if dims[phase] == 1:
+                assert [o[1] for o in ph] == [lm.HALO_FILL]
+                continue
+            assert [o[1] for o in ph] == [lm.HALO_SEND, lm.HALO_SEND, lm.HALO_RECV, lm.HALO_RECV]
+            for k, o in enumerate(o for o in ph if o[1] == lm.HALO_RECV):
+                peer = o[2]
+                prev_from_peer = [q for q in ph if q[1] == lm.HALO_RECV and q[2] == peer]
+                kth = prev_from_peer.index(o)
+                sends = [q for q in plans[peer] if q[0] == phase and q[1] == lm.HALO_SEND and q[2] == r]
+                s = sends[kth]
+                assert s[6] == o[6]  # same cell count
+                if phase == 0:  # column: receiver x=-1 <- sender's last column
+                    assert (o[4], s[4]) in ((-1, lay[peer].w - 1), (lay[r].w, 0))
+                else:
+                    assert (o[4], s[4]) in ((0, lay[peer].h), (lay[r].h + 1, 1))
