@@ -56,43 +56,55 @@ void life_dims_create(int n, int dims[2]);
 /* One halo-exchange operation of a shard (replaces exchange_columns /
  * exchange_rows / exchange_corners, life_cart.c:225-279, and the 1-D ring
  * exchange of 5-gather/life_mpi.c:181-191).  Coordinates are the shard's
- * LOCAL padded frame: owned cells x in [0,w), padded rows 1..h; the one-cell
- * apron is x = -1 / x = w and padded rows 0 / h+1. */
+ * LOCAL frame: owned cells x in [0,w), y in [0,h); padded row of owned row y
+ * is y + yapron; the apron is x in [-xapron, 0) u [w, w+xapron) and rows
+ * y in [-yapron, 0) u [h, h+yapron) (see life_layout). */
 #define LIFE_HALO_SEND 0
 #define LIFE_HALO_RECV 1
-#define LIFE_HALO_FILL 2   /* periodic wrap inside the shard (dims[d] == 1) */
-#define LIFE_HALO_COLUMN 0 /* one cell per padded row: rows [first, first+count) at x = index */
-#define LIFE_HALO_ROW 1    /* contiguous cells x in [first, first+count) of padded row index */
+#define LIFE_HALO_FILL 2   /* axis not partitioned (dims[d] == 1): wrapped inside the shard */
+#define LIFE_HALO_COLUMN 0 /* cells x in [index, index+width) of padded rows [first, first+count) */
+#define LIFE_HALO_ROW 1    /* padded rows [index, index+width), cells x in [first, first+count) */
 typedef struct {
     int32_t phase; /* 0: x (columns) first, then 1: y (rows incl. corners) */
     int32_t kind;  /* LIFE_HALO_SEND / RECV / FILL */
     int32_t peer;  /* global shard rank, -1 for FILL */
     int32_t what;  /* LIFE_HALO_COLUMN / LIFE_HALO_ROW */
-    int64_t index; /* column x, or padded row */
-    int64_t first; /* first padded row (column) or first cell x (row) */
-    int64_t count;
+    int64_t index; /* first column x, or first padded row */
+    int64_t first; /* first padded row (column op) or first cell x (row op) */
+    int64_t count; /* rows (column op) or cells (row op) */
+    int64_t width; /* columns (column op) or rows (row op) */
 } life_halo_op;
 
-/* Builds the per-generation halo plan of shard `rank` of a dims[0] x dims[1]
+/* Builds the per-exchange halo plan of shard `rank` of a dims[0] x dims[1]
  * periodic Cartesian partition (rank = c0*dims[1] + c1, dim 0 splits x, as
- * MPI_Cart_create(reorder=0) at life_cart.c:119-121).  Writes up to max_ops
- * ops in execution order and returns their number (or LIFE_EINVAL).  Sends
- * to and receives from one peer are matched in issue order. */
-int life_halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank,
+ * MPI_Cart_create(reorder=0) at life_cart.c:119-121) for cell encoding
+ * `kernel` (apron widths from life_layout_query).  Writes up to max_ops ops
+ * in execution order and returns their number (or LIFE_EINVAL).  Sends to
+ * and receives from one peer are matched in issue order. */
+int life_halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int kernel,
                    life_halo_op *ops, int max_ops);
 
-/* Padded layout of a shard as allocated on the device: pitch and x-offset in
- * bytes of a padded row, rows = h + 2.  For the bit encoding x-offset is the
- * byte offset of the word holding cell 0. */
+/* Padded layout of a shard as allocated on the device: rows = h + 2*yapron
+ * padded rows of `pitch` bytes; owned cell (x, y) lives in padded row
+ * y + yapron at cell offset x from byte `xoff` (bit encoding: bit x&31 of the
+ * little-endian dword (x>>5), floor division, counted from xoff).
+ * `generations_per_exchange` is how many generations one halo exchange
+ * feeds: 1 for the one-cell apron, LIFE_TEMPORAL_DEPTH for the bit-packed
+ * temporally blocked stencil (32-cell x-apron, 8-row y-apron). */
+#define LIFE_TEMPORAL_DEPTH 8
 typedef struct {
     int64_t w, h;      /* owned block */
     int64_t x0, y0;    /* global origin of the block */
     int64_t pitch;     /* bytes per padded row */
     int64_t xoff;      /* byte offset of owned cell x = 0 in a padded row */
-    int64_t rows;      /* h + 2 */
-    int64_t units;     /* 16-byte lanes per row the stencil walks */
+    int64_t rows;      /* h + 2*yapron */
+    int64_t units;     /* 16-byte lanes per row the one-generation stencil walks */
+    int64_t xapron;    /* apron width in cells (x) */
+    int64_t yapron;    /* apron depth in rows (y) */
     int32_t kernel;    /* LIFE_KERNEL_* */
     int32_t coords[2]; /* Cartesian coordinates of the shard */
+    int32_t generations_per_exchange;
+    int32_t reserved;
 } life_layout;
 
 int life_layout_query(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int kernel,
@@ -133,7 +145,9 @@ int life_dev_upload(life_dev *d, const uint8_t *grid);
 int life_dev_fill_random(life_dev *d, uint64_t seed, uint32_t thr32);
 
 /* `generations` x (life_exchange + life_step): life_cart.c:73-74
- * (replaces life_exchange :275-279 and life_step :189-215). Asynchronous. */
+ * (replaces life_exchange :275-279 and life_step :189-215). Asynchronous.
+ * With a temporally blocked layout, up to generations_per_exchange
+ * generations run per launch and the halo is exchanged once per launch. */
 int life_dev_step(life_dev *d, int64_t generations);
 
 /* life_collect (life_cart.c:281-305; MPI_Gather in 5-gather/life_mpi.c:177-179):
@@ -162,6 +176,11 @@ int life_dev_kernel_stats(life_dev *d, double *avg_ms, int64_t *launches, double
  * keeps the current value.  Defaults come from measurement;
  * LIFE_STEP_ROWS / LIFE_STEP_DEPTH override them at load time. */
 int life_tune(int kernel, int rows, int depth);
+
+/* Temporal (bit, generations_per_exchange > 1) tile height: registers rows
+ * per lane, 48/64/80/96 (tile = rows - 2*LIFE_TEMPORAL_DEPTH owned rows);
+ * 0 keeps the current value; LIFE_TEMPORAL_ROWS overrides at load time. */
+int life_tune_temporal(int rows);
 
 /* life_free (life_cart.c:146-157). */
 void life_dev_destroy(life_dev *d);

@@ -104,18 +104,6 @@ namespace {
 
 life::Wrap wrap_of(const life_dev *d) { return life::Wrap{d->dims[0] == 1, d->dims[1] == 1}; }
 
-// Byte range of the row cells [first, first+count) of a padded row.
-void row_span(const life_layout &L, int64_t first, int64_t count, int64_t *off, int64_t *bytes) {
-    if (L.kernel == LIFE_KERNEL_BIT) {
-        const int64_t w0 = first >> 5, w1 = (first + count - 1) >> 5;  // floor division
-        *off = L.xoff + 4 * w0;
-        *bytes = 4 * (w1 - w0 + 1);
-    } else {
-        *off = L.xoff + first;
-        *bytes = count;
-    }
-}
-
 int shard_alloc(life_dev *d, Shard &s) {
     HIPCHK(hipSetDevice(s.device));
     const size_t bytes = (size_t)(s.lay.pitch * s.lay.rows);
@@ -128,12 +116,13 @@ int shard_alloc(life_dev *d, Shard &s) {
     HIPCHK(hipEventCreateWithFlags(&s.ev_ring, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&s.ev_halo, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&s.ev_sync, hipEventDisableTiming));
-    HIPCHK(hipMalloc(&s.col_send, (size_t)(2 * s.lay.h)));
-    HIPCHK(hipMalloc(&s.col_recv, (size_t)(2 * s.lay.h)));
+    const size_t col_bytes = (size_t)(2 * s.lay.h * life::column_bytes_per_row(s.lay));
+    HIPCHK(hipMalloc(&s.col_send, col_bytes));
+    HIPCHK(hipMalloc(&s.col_recv, col_bytes));
     HIPCHK(hipMalloc(&s.d_count, sizeof(unsigned long long)));
     HIPCHK(hipMalloc(&s.sink, 1024));
     life_halo_op ops[16];
-    const int n = life_halo_plan(d->nx, d->ny, d->dims[0], d->dims[1], s.rank, ops, 16);
+    const int n = life_halo_plan(d->nx, d->ny, d->dims[0], d->dims[1], s.rank, d->kernel, ops, 16);
     if (n < 0) {
         set_err("halo plan failed for shard %d", s.rank);
         return LIFE_EINVAL;
@@ -178,17 +167,19 @@ Shard *find_local(life_dev *d, int rank) {
     return nullptr;
 }
 
-// Pointer + size of the k-th (0-based, per phase) send/recv buffer of op `o`.
+// Pointer + size of the message of op `o` (the slot-th send or recv of its
+// phase): column ops go through the staging slots, row ops are whole padded
+// rows sent straight from / received straight into the buffer (every shard
+// of one Cartesian column has the same pitch).
 void op_buffer(const Shard &s, const life_halo_op &o, int slot, uint8_t *base, uint8_t **ptr, size_t *bytes) {
     if (o.what == LIFE_HALO_COLUMN) {
+        const size_t per = (size_t)(s.lay.h * life::column_bytes_per_row(s.lay));
         uint8_t *st = o.kind == LIFE_HALO_SEND ? s.col_send : s.col_recv;
-        *ptr = st + (size_t)(slot * s.lay.h);
-        *bytes = (size_t)s.lay.h;
+        *ptr = st + (size_t)slot * per;
+        *bytes = per;
     } else {
-        int64_t off, nb;
-        row_span(s.lay, o.first, o.count, &off, &nb);
-        *ptr = base + o.index * s.lay.pitch + off;
-        *bytes = (size_t)nb;
+        *ptr = base + o.index * s.lay.pitch;
+        *bytes = (size_t)(o.width * s.lay.pitch);
     }
 }
 
@@ -325,6 +316,81 @@ int harvest_timers(life_dev *d) {
         }
         s.timers_used = 0;
     }
+    return LIFE_OK;
+}
+
+bool temporal(const life_dev *d) { return d->shards[0].lay.generations_per_exchange > 1; }
+
+// Launches one tile region of the temporal stencil (m generations, cur -> nxt).
+int launch_tiles(life_dev *d, Shard &s, const life::TileRegion &r, int m, bool timed) {
+    const uint8_t *in = s.buf[s.cur];
+    uint8_t *out = s.buf[s.cur ^ 1];
+    TimedLaunch *t = nullptr;
+    if (d->timing && timed) {
+        if (s.timers_used == s.timers.size()) {
+            TimedLaunch n;
+            HIPCHK(hipEventCreate(&n.a));
+            HIPCHK(hipEventCreate(&n.b));
+            s.timers.push_back(n);
+        }
+        t = &s.timers[s.timers_used++];
+        HIPCHK(hipEventRecord(t->a, s.stream));
+    }
+    HIPCHK(life::launch_tstep(s.lay, in, out, r, m, wrap_of(d), s.stream));
+    if (t) {
+        HIPCHK(hipEventRecord(t->b, s.stream));
+        const life::TileGeom g = life::tile_geom(s.lay);
+        const int64_t W = s.lay.w / 32;
+        const int64_t wa = r.tx0 * g.words, wb = r.tx1 * g.words < W ? r.tx1 * g.words : W;
+        const int64_t ya = r.ty0 * g.rows, yb = r.ty1 * g.rows < s.lay.h ? r.ty1 * g.rows : s.lay.h;
+        // algorithmic bytes of the cell-updates this launch performs (0.25 B each)
+        d->acc_bytes += (double)(wb - wa) * 32.0 * (double)(yb - ya) * (double)m * 0.25;
+    }
+    return LIFE_OK;
+}
+
+// m <= K generations of the temporally blocked bit stencil on every shard,
+// then one K-deep halo exchange (the ring tiles first, the exchange of the
+// new state on the comm stream overlapped with the interior tiles).
+int generation_block(life_dev *d, int m) {
+    const bool rx = d->dims[0] > 1, ry = d->dims[1] > 1;
+    if (!(rx || ry)) {
+        for (Shard &s : d->shards) {
+            HIPCHK(hipSetDevice(s.device));
+            const life::TileGeom g = life::tile_geom(s.lay);
+            CHK(launch_tiles(d, s, life::TileRegion{0, g.ntx, 0, g.nty}, m, true));
+        }
+        for (Shard &s : d->shards) s.cur ^= 1;
+        return LIFE_OK;
+    }
+    for (Shard &s : d->shards) {
+        HIPCHK(hipSetDevice(s.device));
+        const life::TileGeom g = life::tile_geom(s.lay);
+        const int64_t TX = g.ntx, TY = g.nty;
+        const int64_t ra = ry ? 1 : 0, rb = ry ? TY - 1 : TY;
+        if (ry) {
+            CHK(launch_tiles(d, s, life::TileRegion{0, TX, 0, 1}, m, false));
+            if (TY > 1) CHK(launch_tiles(d, s, life::TileRegion{0, TX, TY - 1, TY}, m, false));
+        }
+        if (rx && rb > ra) {
+            CHK(launch_tiles(d, s, life::TileRegion{0, 1, ra, rb}, m, false));
+            if (TX > 1) CHK(launch_tiles(d, s, life::TileRegion{TX - 1, TX, ra, rb}, m, false));
+        }
+        HIPCHK(hipEventRecord(s.ev_ring, s.stream));
+        HIPCHK(hipStreamWaitEvent(s.comm_stream, s.ev_ring, 0));
+    }
+    CHK(exchange(d, 1, true));
+    for (Shard &s : d->shards) {
+        HIPCHK(hipSetDevice(s.device));
+        const life::TileGeom g = life::tile_geom(s.lay);
+        const int64_t TX = g.ntx, TY = g.nty;
+        const int64_t ra = ry ? 1 : 0, rb = ry ? TY - 1 : TY;
+        const int64_t ua = rx ? 1 : 0, ub = rx ? TX - 1 : TX;
+        if (rb > ra && ub > ua) CHK(launch_tiles(d, s, life::TileRegion{ua, ub, ra, rb}, m, true));
+        HIPCHK(hipEventRecord(s.ev_halo, s.comm_stream));
+        HIPCHK(hipStreamWaitEvent(s.stream, s.ev_halo, 0));
+    }
+    for (Shard &s : d->shards) s.cur ^= 1;
     return LIFE_OK;
 }
 
@@ -544,6 +610,12 @@ int life_dev_fill_random(life_dev *d, uint64_t seed, uint32_t thr32) {
 
 int life_dev_step(life_dev *d, int64_t generations) {
     if (!d || generations < 0) return LIFE_EINVAL;
+    if (temporal(d)) {
+        const int K = d->shards[0].lay.generations_per_exchange;
+        for (int64_t g = 0; g < generations; g += K)
+            CHK(generation_block(d, (int)(generations - g < K ? generations - g : K)));
+        return LIFE_OK;
+    }
     for (int64_t g = 0; g < generations; g++) CHK(generation(d));
     return LIFE_OK;
 }
@@ -673,6 +745,12 @@ int life_tune(int kernel, int rows, int depth) {
         kernel < -1 || kernel > LIFE_KERNEL_BIT)
         return LIFE_EINVAL;
     life::set_step_tuning(kernel, rows, depth);
+    return LIFE_OK;
+}
+
+int life_tune_temporal(int rows) {
+    if (rows && rows != 48 && rows != 64 && rows != 80 && rows != 96) return LIFE_EINVAL;
+    life::set_temporal_rows(rows);
     return LIFE_OK;
 }
 

@@ -22,7 +22,7 @@ struct StepArgs {
     const uint8_t *in;
     uint8_t *out;
     uint8_t *sink;  // >= 1 KiB scratch: stores of lanes outside the region land here
-    int64_t pitch, xoff, units, w, h;
+    int64_t pitch, xoff, units, w, h, ya;
     int64_t u0, u1, r0, r1, nbx;
     int32_t wrapy;
 };
@@ -46,9 +46,26 @@ struct StepTuning {
 StepTuning step_tuning(bool bit);
 void set_step_tuning(int kernel, int rows, int depth);  // kernel -1: both
 
-// Column halo staging: pack writes column w-1 to stage[0..h) and column 0 to
-// stage[h..2h) (1 byte 0/1 per row); unpack writes stage[0..h) to x = -1 and
-// stage[h..2h) to x = w.
+// Temporally blocked bit stencil (layouts with generations_per_exchange ==
+// LIFE_TEMPORAL_DEPTH): tiles of 62 words x `rows` rows, m <= K generations
+// per launch from `in` to `out`.
+struct TileRegion {
+    int64_t tx0, tx1, ty0, ty1;
+};
+struct TileGeom {
+    int64_t words, rows, ntx, nty;
+};
+TileGeom tile_geom(const life_layout &L);
+hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, const TileRegion &r, int m,
+                        Wrap wrap, hipStream_t s);
+int temporal_rows();              // registers rows per lane (48/64/80/96)
+void set_temporal_rows(int nr);
+
+// Column halo staging: pack writes the last xapron columns to slot 0 and the
+// first xapron columns to slot 1 (h rows each: 1 byte 0/1 per row for a cell
+// column, the dword per row for a bit-encoded word column); unpack writes
+// slot 0 into x in [-xapron, 0) and slot 1 into [w, w + xapron).
+inline int64_t column_bytes_per_row(const life_layout &L) { return L.xapron == 32 ? 4 : 1; }
 hipError_t launch_pack_columns(const life_layout &L, const uint8_t *buf, uint8_t *stage,
                                hipStream_t s);
 hipError_t launch_unpack_columns(const life_layout &L, uint8_t *buf, const uint8_t *stage,

@@ -18,7 +18,9 @@
 //    v_alignbyte, 9-cell sum n9 <= 9 per byte, rule ((n9 - c) | c) == 3.
 //  * BitEnc: 1 bit per cell, 32 cells per dword, x = bit 0 upward.
 //    Horizontal (L,C,R) full adder -> 2-bit sum per row; three rows add to
-//    n9 = u0 + 2*S; alive' = (n9 == 3) | (alive & n9 == 4).
+//    n9 = u0 + 2*S; alive' = (n9 == 3) | (alive & n9 == 4).  Every boolean
+//    step is one v_bitop3_b32 (6 ops per row sum incl. 2 DPP moves, 8 for
+//    the rule).
 #include "life_kernels.h"
 
 #include <stdlib.h>
@@ -73,6 +75,20 @@ struct ByteEnc {
     }
 };
 
+// v_bitop3_b32 (gfx950): any 3-input bitwise function in one VALU op.  The
+// truth table is indexed by {S0,S1,S2} with S0 the most significant bit, so
+// the immediate of f is f(0xF0, 0xCC, 0xAA).
+template <uint32_t IMM>
+__device__ __forceinline__ uint32_t b3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, IMM);
+}
+constexpr uint32_t kXor3 = 0xF0 ^ 0xCC ^ 0xAA;                          // a ^ b ^ c
+constexpr uint32_t kMaj = (0xF0 & 0xCC) | (0xF0 & 0xAA) | (0xCC & 0xAA);  // majority
+constexpr uint32_t kEq1 = ((0xF0 ^ 0xCC) & ~0xAA) & 0xFF;                // (v0^k0) & ~v1
+constexpr uint32_t kEq2 = (~(0xF0 ^ 0xCC) & (0xAA ^ (0xF0 & 0xCC))) & 0xFF;  // ~(v0^k0) & (v1^(v0&k0))
+constexpr uint32_t kMux = ((0xF0 & 0xCC) | (~0xF0 & 0xAA)) & 0xFF;       // a ? b : c
+constexpr uint32_t kAndOr = (0xF0 & (0xCC | 0xAA)) & 0xFF;               // a & (b | c)
+
 struct BitEnc {
     static constexpr int64_t kCellsPerUnit = 128;
     static constexpr uint32_t kCell0 = 1u;
@@ -82,11 +98,11 @@ struct BitEnc {
     struct H {
         uint32_t s0[4], s1[4];
     };
+    // full adder: L + C + R = s0 + 2*s1
     static __device__ __forceinline__ void fa(uint32_t L, uint32_t C, uint32_t R, uint32_t &s0,
                                               uint32_t &s1) {
-        const uint32_t t = L ^ C;
-        s0 = t ^ R;
-        s1 = (t & R) | (~t & L);  // majority (v_bfi_b32)
+        s0 = b3<kXor3>(L, C, R);
+        s1 = b3<kMaj>(L, C, R);
     }
     static __device__ __forceinline__ H hsum(uint4 d, uint32_t l, uint32_t r) {
         H h;
@@ -96,16 +112,17 @@ struct BitEnc {
         fa(__builtin_amdgcn_alignbit(d.w, d.z, 31), d.w, __builtin_amdgcn_alignbit(r, d.w, 1), h.s0[3], h.s1[3]);
         return h;
     }
+    // Rows a, b, c (2-bit horizontal sums) -> next state of the centre row.
+    // n9 = (a0+b0+c0) + 2(a1+b1+c1) = u0 + 2*S with S = v0 + k0 + 2*v1;
+    // alive' = (n9 == 3) | (alive & n9 == 4) = u0 ? S==1 : (alive & S==2).
     static __device__ __forceinline__ uint32_t rule1(uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1,
                                                      uint32_t c0, uint32_t c1, uint32_t alive) {
-        uint32_t u0, k0, v0, v1;
-        fa(a0, b0, c0, u0, k0);  // bit-0 column: u0 + 2*k0
-        fa(a1, b1, c1, v0, v1);  // bit-1 column: v0 + 2*v1 (weight 2)
-        // n9 = u0 + 2*S, S = v0 + k0 + 2*v1 = p + 2*(q + v1)
-        const uint32_t p = v0 ^ k0, q = v0 & k0;
-        const uint32_t eq1 = p & ~(v1 | q);   // S == 1
-        const uint32_t eq2 = ~p & (v1 ^ q);   // S == 2
-        return (u0 & eq1) | (~u0 & alive & eq2);  // n9 == 3  |  (alive & n9 == 4)
+        const uint32_t u0 = b3<kXor3>(a0, b0, c0), k0 = b3<kMaj>(a0, b0, c0);
+        const uint32_t v0 = b3<kXor3>(a1, b1, c1), v1 = b3<kMaj>(a1, b1, c1);
+        const uint32_t eq1 = b3<kEq1>(v0, k0, v1);  // S == 1
+        const uint32_t eq2 = b3<kEq2>(v0, k0, v1);  // S == 2
+        const uint32_t e = b3<kMux>(u0, eq1, eq2);
+        return b3<kAndOr>(e, u0, alive);  // u0 ? eq1 : (alive & eq2)
     }
     static __device__ __forceinline__ uint4 rule(const H &a, const H &b, const H &c, uint4 v) {
         uint4 o;
@@ -125,7 +142,7 @@ struct BitEnc {
 // below really keeps D rows of loads in flight.
 struct Lane {
     const uint8_t *in;
-    int64_t pitch, h;
+    int64_t pitch, h, ya;
     int64_t off;        // byte offset of the (clamped) unit in a padded row
     int64_t exoff;      // extra dword: left (lane 0), right (lane 63), wrap-left (unit 0)
     uint32_t exshift;   // wrap-left: move cell w-1 to the top position of the dword
@@ -136,11 +153,11 @@ struct Lane {
     bool wrapy;
 };
 
-__device__ __forceinline__ const uint8_t *row_ptr(const Lane &c, int64_t p) {
-    // padded row p in [0, h+1]; with a periodic y axis inside the shard the
+__device__ __forceinline__ const uint8_t *row_ptr(const Lane &c, int64_t y) {
+    // owned row y in [-1, h]; with a periodic y axis inside the shard the
     // apron rows are the opposite owned rows (ind() wrap, life_cart.c:11).
-    if (c.wrapy) p = p == 0 ? c.h : (p == c.h + 1 ? 1 : p);
-    return c.in + p * c.pitch;
+    if (c.wrapy) y = y < 0 ? y + c.h : (y >= c.h ? y - c.h : y);
+    return c.in + (y + c.ya) * c.pitch;
 }
 
 struct RowData {
@@ -149,8 +166,8 @@ struct RowData {
 };
 
 template <bool WRAPX>
-__device__ __forceinline__ RowData load_row(const Lane &c, int64_t p) {
-    const uint8_t *row = row_ptr(c, p);
+__device__ __forceinline__ RowData load_row(const Lane &c, int64_t y) {
+    const uint8_t *row = row_ptr(c, y);
     RowData r;
     r.d = *reinterpret_cast<const uint4 *>(row + c.off);
     r.ex = *reinterpret_cast<const uint32_t *>(row + c.exoff);
@@ -174,20 +191,20 @@ __device__ __forceinline__ typename E::H row_sum(const Lane &c, RowData &r) {
     return E::hsum(r.d, from_left(ex, r.d.w), right);
 }
 
-// N output rows starting at owned row ys (padded rows ys .. ys+N+1 are read),
+// N output rows starting at owned row ys (owned rows ys-1 .. ys+N are read),
 // D rows of loads kept in flight.
 template <class E, int N, int D, bool WRAPX>
 __device__ __forceinline__ void strip_full(const Lane &c, int64_t ys, uint8_t *dst, int64_t spitch) {
     static_assert(D <= N + 2, "prefetch deeper than the strip");
     RowData q[D];
 #pragma unroll
-    for (int k = 0; k < D; ++k) q[k] = load_row<WRAPX>(c, ys + k);
+    for (int k = 0; k < D; ++k) q[k] = load_row<WRAPX>(c, ys - 1 + k);
     typename E::H hp, hc;
     uint4 cc;
 #pragma unroll
     for (int k = 0; k < N + 2; ++k) {
         RowData r = q[k % D];
-        if (k + D < N + 2) q[k % D] = load_row<WRAPX>(c, ys + k + D);
+        if (k + D < N + 2) q[k % D] = load_row<WRAPX>(c, ys - 1 + k + D);
         const typename E::H hn = row_sum<E, WRAPX>(c, r);
         if (k == 0) {
             hp = hn;
@@ -206,14 +223,14 @@ __device__ __forceinline__ void strip_full(const Lane &c, int64_t ys, uint8_t *d
 
 template <class E, bool WRAPX>
 __device__ __forceinline__ void strip_tail(const Lane &c, int64_t ys, int n, uint8_t *dst, int64_t spitch) {
-    RowData r = load_row<WRAPX>(c, ys);
+    RowData r = load_row<WRAPX>(c, ys - 1);
     typename E::H hp = row_sum<E, WRAPX>(c, r);
-    r = load_row<WRAPX>(c, ys + 1);
+    r = load_row<WRAPX>(c, ys);
     typename E::H hc = row_sum<E, WRAPX>(c, r);
     uint4 cc = r.d;
 #pragma unroll 1
     for (int i = 0; i < n; ++i) {
-        r = load_row<WRAPX>(c, ys + 2 + i);
+        r = load_row<WRAPX>(c, ys + 1 + i);
         const typename E::H hn = row_sum<E, WRAPX>(c, r);
         *reinterpret_cast<uint4 *>(dst) = E::rule(hp, hc, hn, cc);
         dst += spitch;
@@ -227,7 +244,7 @@ template <class E, int R, int D, bool WRAPX>
 __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs a) {
     const int64_t bx = blockIdx.x % a.nbx, by = blockIdx.x / a.nbx;
     const int lane = threadIdx.x & 63;
-    const int64_t wbase = a.u0 + (bx * (kBlock / 64) + (threadIdx.x >> 6)) * 64;
+    const int64_t wbase = a.u0 + (bx * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * 64;
     if (wbase >= a.u1) return;  // the whole wave is right of the region
     const int64_t ys = a.r0 + by * R;
     const int64_t u = wbase + lane;
@@ -236,6 +253,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs a) {
     c.in = a.in;
     c.pitch = a.pitch;
     c.h = a.h;
+    c.ya = a.ya;
     c.wrapy = a.wrapy != 0;
     c.xoff = a.xoff;
     c.off = a.xoff + 16 * uc;
@@ -268,13 +286,100 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs a) {
         }
     }
     const bool st = u < a.u1;
-    uint8_t *dst = st ? a.out + (ys + 1) * a.pitch + a.xoff + 16 * u : a.sink + 16 * lane;
+    uint8_t *dst = st ? a.out + (ys + a.ya) * a.pitch + a.xoff + 16 * u : a.sink + 16 * lane;
     const int64_t spitch = st ? a.pitch : 0;
     const int64_t n = a.r1 - ys < R ? a.r1 - ys : R;
     if (n == R)
         strip_full<E, R, D, WRAPX>(c, ys, dst, spitch);
     else
         strip_tail<E, WRAPX>(c, ys, (int)n, dst, spitch);
+}
+
+// ------------------------------------------------------------------ temporal
+// Temporally blocked bit stencil (layouts with generations_per_exchange > 1).
+// One wave owns a tile of 62 word columns x T rows: lane l holds word column
+// 62*tx + l - 1 (lanes 0 and 63 are the one-word x-apron of the tile) for
+// NR = T + 2K consecutive rows in NR registers, runs m <= K generations
+// there, and stores rows [K, K+T) of lanes 1..62.  After m generations the
+// wrong values that enter at the tile's edge rows / edge lanes have moved m
+// rows / m bits inward: rows [K, K+T) and lanes 1..62 (32 bits of margin) are
+// still exact.  HBM traffic per m generations: NR rows read + T rows written
+// per 62 columns, instead of 2 x m full passes.
+constexpr int kTK = LIFE_TEMPORAL_DEPTH;
+
+struct TArgs {
+    const uint8_t *in;
+    uint8_t *out;
+    int64_t pitch, xoff, W, h, ya;  // W = 32-bit words per owned row
+    int64_t tx0, tx1, ty0, ty1;     // tile region
+    int32_t m;
+};
+
+__device__ __forceinline__ void bit_hsum(uint32_t v, uint32_t &s0, uint32_t &s1) {
+    const uint32_t L = __builtin_amdgcn_alignbit(v, from_left(0u, v), 31);
+    const uint32_t R = __builtin_amdgcn_alignbit(from_right(0u, v), v, 1);
+    BitEnc::fa(L, v, R, s0, s1);
+}
+
+template <int NR, bool WRAPX, bool WRAPY>
+__global__ __launch_bounds__(kBlock) void tstep_kernel(TArgs a) {
+    constexpr int T = NR - 2 * kTK;
+    const int lane = threadIdx.x & 63;
+    // wave index: uniform, so every row address below is scalar (SALU) math
+    const int64_t wv = (int64_t)blockIdx.x * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t ntx = a.tx1 - a.tx0;
+    const int64_t tx = a.tx0 + wv % ntx, ty = a.ty0 + wv / ntx;
+    if (ty >= a.ty1) return;  // whole wave
+    const int64_t j = tx * 62 + lane - 1;  // word column of this lane
+    int64_t jl;
+    if (WRAPX) {
+        jl = j % a.W;
+        if (jl < 0) jl += a.W;
+    } else {
+        jl = j > a.W ? a.W : j;  // words -1 .. W hold cells/apron; beyond: clamp (never stored)
+    }
+    const uint32_t voff = (uint32_t)(a.xoff + 4 * jl);
+    // first register row = owned row ty*T - K
+    int64_t y = ty * T - kTK;
+    if (WRAPY) {
+        y %= a.h;
+        if (y < 0) y += a.h;
+    }
+    uint32_t v[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        int64_t yy = y;
+        if (!WRAPY) yy = y < -kTK ? -kTK : (y >= a.h + kTK ? a.h + kTK - 1 : y);
+        v[r] = *reinterpret_cast<const uint32_t *>(a.in + (yy + a.ya) * a.pitch + voff);
+        ++y;
+        if (WRAPY && y == a.h) y = 0;
+    }
+    for (int g = 0; g < a.m; ++g) {
+        uint32_t p0 = 0u, p1 = 0u, c0, c1;  // row -1 of the tile counts as dead
+        bit_hsum(v[0], c0, c1);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            uint32_t n0 = 0u, n1 = 0u;
+            if (r + 1 < NR) bit_hsum(v[r + 1], n0, n1);
+            v[r] = BitEnc::rule1(p0, p1, c0, c1, n0, n1, v[r]);
+            p0 = c0;
+            p1 = c1;
+            c0 = n0;
+            c1 = n1;
+        }
+    }
+    const bool st = lane >= 1 && lane <= 62 && j < a.W;
+    const int64_t yo = ty * T;  // owned row of register row K
+    uint8_t *dst = a.out + (yo + a.ya) * a.pitch + voff;
+    if (yo + T <= a.h) {
+#pragma unroll
+        for (int r = 0; r < T; ++r)
+            if (st) *reinterpret_cast<uint32_t *>(dst + r * a.pitch) = v[kTK + r];
+    } else {
+#pragma unroll
+        for (int r = 0; r < T; ++r)
+            if (st && yo + r < a.h) *reinterpret_cast<uint32_t *>(dst + r * a.pitch) = v[kTK + r];
+    }
 }
 
 // ------------------------------------------------------------------ cell access
@@ -295,28 +400,42 @@ __device__ __forceinline__ void set_cell(uint8_t *row, int64_t xoff, int64_t x, 
     w[x >> 5] = (w[x >> 5] & ~m) | (v ? m : 0u);
 }
 
-__global__ void pack_columns_kernel(const uint8_t *buf, int64_t pitch, int64_t xoff, int64_t w, int64_t h,
-                                    uint8_t *stage, bool bit) {
+// Column halo staging.  Cell columns (xapron == 1): one byte 0/1 per row.
+// Word columns (bit encoding, xapron == 32): the whole dword per row.
+__global__ void pack_columns_kernel(const uint8_t *buf, int64_t pitch, int64_t ya, int64_t xoff, int64_t w,
+                                    int64_t h, int64_t xa, uint8_t *stage, bool bit) {
     const int64_t y = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (y >= h) return;
-    const uint8_t *row = buf + (y + 1) * pitch;
+    const uint8_t *row = buf + (y + ya) * pitch;
+    if (xa == 32) {
+        const uint32_t *wd = reinterpret_cast<const uint32_t *>(row + xoff);
+        reinterpret_cast<uint32_t *>(stage)[y] = wd[(w - 32) >> 5];
+        reinterpret_cast<uint32_t *>(stage)[h + y] = wd[0];
+        return;
+    }
     stage[y] = (uint8_t)get_cell(row, xoff, w - 1, bit);
     stage[h + y] = (uint8_t)get_cell(row, xoff, 0, bit);
 }
 
-__global__ void unpack_columns_kernel(uint8_t *buf, int64_t pitch, int64_t xoff, int64_t w, int64_t h,
-                                      const uint8_t *stage, bool bit) {
+__global__ void unpack_columns_kernel(uint8_t *buf, int64_t pitch, int64_t ya, int64_t xoff, int64_t w,
+                                      int64_t h, int64_t xa, const uint8_t *stage, bool bit) {
     const int64_t y = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (y >= h) return;
-    uint8_t *row = buf + (y + 1) * pitch;
+    uint8_t *row = buf + (y + ya) * pitch;
+    if (xa == 32) {
+        uint32_t *wd = reinterpret_cast<uint32_t *>(row + xoff);
+        wd[-1] = reinterpret_cast<const uint32_t *>(stage)[y];
+        wd[w >> 5] = reinterpret_cast<const uint32_t *>(stage)[h + y];
+        return;
+    }
     set_cell(row, xoff, -1, stage[y] ? 1u : 0u, bit);
     set_cell(row, xoff, w, stage[h + y] ? 1u : 0u, bit);
 }
 
 // One thread per 16-byte unit of an owned row: dense (row pitch w) -> padded.
 template <int CPU>  // cells per unit: 16 (byte) or 128 (bit)
-__global__ void import_kernel(const uint8_t *dense, uint8_t *buf, int64_t pitch, int64_t xoff, int64_t w,
-                              int64_t h, int64_t units) {
+__global__ void import_kernel(const uint8_t *dense, uint8_t *buf, int64_t pitch, int64_t ya, int64_t xoff,
+                              int64_t w, int64_t h, int64_t units) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= units * h) return;
     const int64_t u = i % units, y = i / units;
@@ -332,17 +451,17 @@ __global__ void import_kernel(const uint8_t *dense, uint8_t *buf, int64_t pitch,
         else
             word[k >> 5] |= v << (k & 31);
     }
-    *reinterpret_cast<uint4 *>(buf + (y + 1) * pitch + xoff + 16 * u) =
+    *reinterpret_cast<uint4 *>(buf + (y + ya) * pitch + xoff + 16 * u) =
         make_uint4(word[0], word[1], word[2], word[3]);
 }
 
 template <int CPU>
-__global__ void export_kernel(const uint8_t *buf, uint8_t *dense, int64_t pitch, int64_t xoff, int64_t w,
-                              int64_t h, int64_t units) {
+__global__ void export_kernel(const uint8_t *buf, uint8_t *dense, int64_t pitch, int64_t ya, int64_t xoff,
+                              int64_t w, int64_t h, int64_t units) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= units * h) return;
     const int64_t u = i % units, y = i / units;
-    const uint4 q = *reinterpret_cast<const uint4 *>(buf + (y + 1) * pitch + xoff + 16 * u);
+    const uint4 q = *reinterpret_cast<const uint4 *>(buf + (y + ya) * pitch + xoff + 16 * u);
     const uint32_t word[4] = {q.x, q.y, q.z, q.w};
     uint8_t *o = dense + y * w;
     const int64_t x0 = u * CPU;
@@ -362,7 +481,7 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
 }
 
 template <int CPU>
-__global__ void fill_random_kernel(uint8_t *buf, int64_t pitch, int64_t xoff, int64_t w, int64_t h,
+__global__ void fill_random_kernel(uint8_t *buf, int64_t pitch, int64_t ya, int64_t xoff, int64_t w, int64_t h,
                                    int64_t units, int64_t gx0, int64_t gy0, int64_t nx, uint64_t key,
                                    uint32_t thr) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -380,18 +499,18 @@ __global__ void fill_random_kernel(uint8_t *buf, int64_t pitch, int64_t xoff, in
         else
             word[k >> 5] |= v << (k & 31);
     }
-    *reinterpret_cast<uint4 *>(buf + (y + 1) * pitch + xoff + 16 * u) =
+    *reinterpret_cast<uint4 *>(buf + (y + ya) * pitch + xoff + 16 * u) =
         make_uint4(word[0], word[1], word[2], word[3]);
 }
 
 template <int CPU>
-__global__ void live_count_kernel(const uint8_t *buf, int64_t pitch, int64_t xoff, int64_t w, int64_t h,
+__global__ void live_count_kernel(const uint8_t *buf, int64_t pitch, int64_t ya, int64_t xoff, int64_t w, int64_t h,
                                   int64_t units, unsigned long long *count) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long c = 0;
     if (i < units * h) {
         const int64_t u = i % units, y = i / units;
-        const uint4 q = *reinterpret_cast<const uint4 *>(buf + (y + 1) * pitch + xoff + 16 * u);
+        const uint4 q = *reinterpret_cast<const uint4 *>(buf + (y + ya) * pitch + xoff + 16 * u);
         const uint32_t word[4] = {q.x, q.y, q.z, q.w};
         const int64_t valid = w - u * CPU;  // cells of this unit inside the block
         constexpr int kPerWord = CPU / 4;
@@ -422,11 +541,14 @@ namespace {
 // byte R64/D2 were the fastest of {16,32,64} x {2,4,8}.
 struct Tunings {
     StepTuning t[2];  // [0] byte, [1] bit
+    int nr = 80;      // temporal tile: registers rows per lane (T = nr - 2K); 80 and 96
+                      // tied fastest at 65536^2 (profiles/r01/tune_temporal.jsonl)
     Tunings() : t{{64, 2}, {16, 8}} {
         for (StepTuning &v : t) {
             if (const char *e = getenv("LIFE_STEP_ROWS")) v.rows = atoi(e);
             if (const char *e = getenv("LIFE_STEP_DEPTH")) v.depth = atoi(e);
         }
+        if (const char *e = getenv("LIFE_TEMPORAL_ROWS")) nr = atoi(e);
     }
 };
 Tunings &tunings() {
@@ -436,6 +558,15 @@ Tunings &tunings() {
 }  // namespace
 
 StepTuning step_tuning(bool bit) { return tunings().t[bit ? 1 : 0]; }
+
+int temporal_rows() {
+    const int nr = tunings().nr;
+    return nr == 48 || nr == 64 || nr == 96 ? nr : 80;
+}
+
+void set_temporal_rows(int nr) {
+    if (nr == 48 || nr == 64 || nr == 80 || nr == 96) tunings().nr = nr;
+}
 
 void set_step_tuning(int kernel, int rows, int depth) {
     for (int k = 0; k < 2; k++) {
@@ -488,6 +619,7 @@ hipError_t launch_step(const life_layout &L, const uint8_t *in, uint8_t *out, ui
     a.units = L.units;
     a.w = L.w;
     a.h = L.h;
+    a.ya = L.yapron;
     a.u0 = reg.u0;
     a.u1 = reg.u1;
     a.r0 = reg.r0;
@@ -499,32 +631,85 @@ hipError_t launch_step(const life_layout &L, const uint8_t *in, uint8_t *out, ui
     return is_bit(L) ? launch_e<BitEnc>(a, t, wrap.x, grid, s) : launch_e<ByteEnc>(a, t, wrap.x, grid, s);
 }
 
+namespace {
+template <int NR>
+hipError_t launch_t(const TArgs &a, Wrap wrap, unsigned grid, hipStream_t s) {
+    if (wrap.x && wrap.y)
+        tstep_kernel<NR, true, true><<<grid, kBlock, 0, s>>>(a);
+    else if (wrap.x)
+        tstep_kernel<NR, true, false><<<grid, kBlock, 0, s>>>(a);
+    else if (wrap.y)
+        tstep_kernel<NR, false, true><<<grid, kBlock, 0, s>>>(a);
+    else
+        tstep_kernel<NR, false, false><<<grid, kBlock, 0, s>>>(a);
+    return hipGetLastError();
+}
+}  // namespace
+
+TileGeom tile_geom(const life_layout &L) {
+    const int nr = temporal_rows();
+    TileGeom g;
+    g.words = 62;
+    g.rows = nr - 2 * kTK;
+    g.ntx = (L.w / 32 + g.words - 1) / g.words;
+    g.nty = (L.h + g.rows - 1) / g.rows;
+    return g;
+}
+
+hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, const TileRegion &r, int m,
+                        Wrap wrap, hipStream_t s) {
+    if (r.tx1 <= r.tx0 || r.ty1 <= r.ty0 || m <= 0) return hipSuccess;
+    if (m > kTK || L.generations_per_exchange != kTK) return hipErrorInvalidValue;
+    TArgs a;
+    a.in = in;
+    a.out = out;
+    a.pitch = L.pitch;
+    a.xoff = L.xoff;
+    a.W = L.w / 32;
+    a.h = L.h;
+    a.ya = L.yapron;
+    a.tx0 = r.tx0;
+    a.tx1 = r.tx1;
+    a.ty0 = r.ty0;
+    a.ty1 = r.ty1;
+    a.m = m;
+    const int64_t waves = (r.tx1 - r.tx0) * (r.ty1 - r.ty0);
+    const unsigned grid = (unsigned)((waves + kBlock / 64 - 1) / (kBlock / 64));
+    switch (temporal_rows()) {
+    case 48: return launch_t<48>(a, wrap, grid, s);
+    case 64: return launch_t<64>(a, wrap, grid, s);
+    case 96: return launch_t<96>(a, wrap, grid, s);
+    default: return launch_t<80>(a, wrap, grid, s);
+    }
+}
+
 hipError_t launch_pack_columns(const life_layout &L, const uint8_t *buf, uint8_t *stage, hipStream_t s) {
-    pack_columns_kernel<<<blocks_for(L.h, 256), 256, 0, s>>>(buf, L.pitch, L.xoff, L.w, L.h, stage, is_bit(L));
+    pack_columns_kernel<<<blocks_for(L.h, 256), 256, 0, s>>>(buf, L.pitch, L.yapron, L.xoff, L.w, L.h, L.xapron,
+                                                              stage, is_bit(L));
     return hipGetLastError();
 }
 
 hipError_t launch_unpack_columns(const life_layout &L, uint8_t *buf, const uint8_t *stage, hipStream_t s) {
-    unpack_columns_kernel<<<blocks_for(L.h, 256), 256, 0, s>>>(buf, L.pitch, L.xoff, L.w, L.h, stage,
-                                                                is_bit(L));
+    unpack_columns_kernel<<<blocks_for(L.h, 256), 256, 0, s>>>(buf, L.pitch, L.yapron, L.xoff, L.w, L.h,
+                                                                L.xapron, stage, is_bit(L));
     return hipGetLastError();
 }
 
 hipError_t launch_import_block(const life_layout &L, const uint8_t *dense, uint8_t *buf, hipStream_t s) {
     const unsigned g = blocks_for(L.units * L.h, 256);
     if (is_bit(L))
-        import_kernel<128><<<g, 256, 0, s>>>(dense, buf, L.pitch, L.xoff, L.w, L.h, L.units);
+        import_kernel<128><<<g, 256, 0, s>>>(dense, buf, L.pitch, L.yapron, L.xoff, L.w, L.h, L.units);
     else
-        import_kernel<16><<<g, 256, 0, s>>>(dense, buf, L.pitch, L.xoff, L.w, L.h, L.units);
+        import_kernel<16><<<g, 256, 0, s>>>(dense, buf, L.pitch, L.yapron, L.xoff, L.w, L.h, L.units);
     return hipGetLastError();
 }
 
 hipError_t launch_export_block(const life_layout &L, const uint8_t *buf, uint8_t *dense, hipStream_t s) {
     const unsigned g = blocks_for(L.units * L.h, 256);
     if (is_bit(L))
-        export_kernel<128><<<g, 256, 0, s>>>(buf, dense, L.pitch, L.xoff, L.w, L.h, L.units);
+        export_kernel<128><<<g, 256, 0, s>>>(buf, dense, L.pitch, L.yapron, L.xoff, L.w, L.h, L.units);
     else
-        export_kernel<16><<<g, 256, 0, s>>>(buf, dense, L.pitch, L.xoff, L.w, L.h, L.units);
+        export_kernel<16><<<g, 256, 0, s>>>(buf, dense, L.pitch, L.yapron, L.xoff, L.w, L.h, L.units);
     return hipGetLastError();
 }
 
@@ -532,10 +717,10 @@ hipError_t launch_fill_random(const life_layout &L, int64_t nx, uint64_t key, ui
                               hipStream_t s) {
     const unsigned g = blocks_for(L.units * L.h, 256);
     if (is_bit(L))
-        fill_random_kernel<128><<<g, 256, 0, s>>>(buf, L.pitch, L.xoff, L.w, L.h, L.units, L.x0, L.y0, nx,
+        fill_random_kernel<128><<<g, 256, 0, s>>>(buf, L.pitch, L.yapron, L.xoff, L.w, L.h, L.units, L.x0, L.y0, nx,
                                                   key, thr32);
     else
-        fill_random_kernel<16><<<g, 256, 0, s>>>(buf, L.pitch, L.xoff, L.w, L.h, L.units, L.x0, L.y0, nx,
+        fill_random_kernel<16><<<g, 256, 0, s>>>(buf, L.pitch, L.yapron, L.xoff, L.w, L.h, L.units, L.x0, L.y0, nx,
                                                  key, thr32);
     return hipGetLastError();
 }
@@ -544,9 +729,9 @@ hipError_t launch_live_count(const life_layout &L, const uint8_t *buf, unsigned 
                              hipStream_t s) {
     const unsigned g = blocks_for(L.units * L.h, 256);
     if (is_bit(L))
-        live_count_kernel<128><<<g, 256, 0, s>>>(buf, L.pitch, L.xoff, L.w, L.h, L.units, count);
+        live_count_kernel<128><<<g, 256, 0, s>>>(buf, L.pitch, L.yapron, L.xoff, L.w, L.h, L.units, count);
     else
-        live_count_kernel<16><<<g, 256, 0, s>>>(buf, L.pitch, L.xoff, L.w, L.h, L.units, count);
+        live_count_kernel<16><<<g, 256, 0, s>>>(buf, L.pitch, L.yapron, L.xoff, L.w, L.h, L.units, count);
     return hipGetLastError();
 }
 

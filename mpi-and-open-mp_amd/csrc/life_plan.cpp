@@ -36,6 +36,25 @@ void life_dims_create(int n, int dims[2]) {
     dims[1] = d1;
 }
 
+// The bit-packed temporally blocked stencil exchanges whole 32-cell words
+// in x and LIFE_TEMPORAL_DEPTH rows in y, and wraps a non-partitioned x axis
+// at word granularity: every block width must be a multiple of 32, and a
+// partitioned y axis needs blocks at least as tall as the apron it feeds.
+static bool temporal_ok(int64_t nx, int64_t ny, int dims0, int dims1) {
+    for (int k = 0; k < dims0; k++) {
+        int64_t s, e;
+        life_decomposition(nx, dims0, k, &s, &e);
+        if ((e - s) % 32 != 0) return false;
+    }
+    if (dims1 > 1)
+        for (int k = 0; k < dims1; k++) {
+            int64_t s, e;
+            life_decomposition(ny, dims1, k, &s, &e);
+            if (e - s < LIFE_TEMPORAL_DEPTH) return false;
+        }
+    return true;
+}
+
 int life_layout_query(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int kernel,
                       life_layout *out) {
     if (!out || nx <= 0 || ny <= 0 || dims0 <= 0 || dims1 <= 0 || rank < 0 ||
@@ -54,57 +73,63 @@ int life_layout_query(int64_t nx, int64_t ny, int dims0, int dims1, int rank, in
     out->kernel = kernel;
     out->coords[0] = c0;
     out->coords[1] = c1;
+    const bool temporal = kernel == LIFE_KERNEL_BIT && temporal_ok(nx, ny, dims0, dims1);
+    out->xapron = temporal ? 32 : 1;
+    out->yapron = temporal ? LIFE_TEMPORAL_DEPTH : 1;
+    out->generations_per_exchange = temporal ? LIFE_TEMPORAL_DEPTH : 1;
     const int64_t cells_per_unit = kernel == LIFE_KERNEL_BIT ? 128 : 16;
     out->units = (out->w + cells_per_unit - 1) / cells_per_unit;
     out->xoff = kXoff;
-    // room for the last unit, the right-apron cell and the right extra dword
+    // room for the last unit, the right apron (cell or word) and the right extra dword
     out->pitch = round_up(kXoff + 16 * out->units + 16, 256);
-    out->rows = out->h + 2;
+    out->rows = out->h + 2 * out->yapron;
     return LIFE_OK;
 }
 
-int life_halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, life_halo_op *ops,
-                   int max_ops) {
+int life_halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int kernel,
+                   life_halo_op *ops, int max_ops) {
     life_layout L;
-    const int rc = life_layout_query(nx, ny, dims0, dims1, rank, LIFE_KERNEL_BYTE, &L);
+    const int rc = life_layout_query(nx, ny, dims0, dims1, rank, kernel, &L);
     if (rc != LIFE_OK) return rc;
     const int c0 = L.coords[0], c1 = L.coords[1];
-    const int64_t w = L.w, h = L.h;
+    const int64_t w = L.w, h = L.h, xa = L.xapron, ya = L.yapron;
     life_halo_op tmp[10];
     int n = 0;
-    auto add = [&](int phase, int kind, int peer, int what, int64_t index, int64_t first, int64_t count) {
+    auto add = [&](int phase, int kind, int peer, int what, int64_t index, int64_t width, int64_t first,
+                   int64_t count) {
         life_halo_op &o = tmp[n++];
         o.phase = phase;
         o.kind = kind;
         o.peer = peer;
         o.what = what;
         o.index = index;
+        o.width = width;
         o.first = first;
         o.count = count;
     };
-    // Phase 0: columns (dim 0 splits x).  MPI_Cart_shift(dim 0): left/right.
+    // Phase 0: columns (dim 0 splits x), owned rows only.  MPI_Cart_shift(dim 0).
     if (dims0 == 1) {
-        add(0, LIFE_HALO_FILL, -1, LIFE_HALO_COLUMN, -1, 1, h);
+        add(0, LIFE_HALO_FILL, -1, LIFE_HALO_COLUMN, -xa, xa, ya, h);
     } else {
         const int right = cart_rank((c0 + 1) % dims0, c1, dims1);
         const int left = cart_rank((c0 - 1 + dims0) % dims0, c1, dims1);
         // life_cart.c:251-254 order: Send right, Recv left, Send left, Recv right.
-        add(0, LIFE_HALO_SEND, right, LIFE_HALO_COLUMN, w - 1, 1, h);
-        add(0, LIFE_HALO_SEND, left, LIFE_HALO_COLUMN, 0, 1, h);
-        add(0, LIFE_HALO_RECV, left, LIFE_HALO_COLUMN, -1, 1, h);
-        add(0, LIFE_HALO_RECV, right, LIFE_HALO_COLUMN, w, 1, h);
+        add(0, LIFE_HALO_SEND, right, LIFE_HALO_COLUMN, w - xa, xa, ya, h);
+        add(0, LIFE_HALO_SEND, left, LIFE_HALO_COLUMN, 0, xa, ya, h);
+        add(0, LIFE_HALO_RECV, left, LIFE_HALO_COLUMN, -xa, xa, ya, h);
+        add(0, LIFE_HALO_RECV, right, LIFE_HALO_COLUMN, w, xa, ya, h);
     }
-    // Phase 1: rows of width+2 (x = -1 .. w), carrying the corners.
+    // Phase 1: whole rows including the x-apron just received (the corners).
     if (dims1 == 1) {
-        add(1, LIFE_HALO_FILL, -1, LIFE_HALO_ROW, 0, -1, w + 2);
+        add(1, LIFE_HALO_FILL, -1, LIFE_HALO_ROW, 0, ya, -xa, w + 2 * xa);
     } else {
         const int right = cart_rank(c0, (c1 + 1) % dims1, dims1);
         const int left = cart_rank(c0, (c1 - 1 + dims1) % dims1, dims1);
-        // life_cart.c:235-238 order.
-        add(1, LIFE_HALO_SEND, right, LIFE_HALO_ROW, h, -1, w + 2);
-        add(1, LIFE_HALO_SEND, left, LIFE_HALO_ROW, 1, -1, w + 2);
-        add(1, LIFE_HALO_RECV, left, LIFE_HALO_ROW, 0, -1, w + 2);
-        add(1, LIFE_HALO_RECV, right, LIFE_HALO_ROW, h + 1, -1, w + 2);
+        // life_cart.c:235-238 order.  Padded row of owned row y is y + ya.
+        add(1, LIFE_HALO_SEND, right, LIFE_HALO_ROW, h, ya, -xa, w + 2 * xa);
+        add(1, LIFE_HALO_SEND, left, LIFE_HALO_ROW, ya, ya, -xa, w + 2 * xa);
+        add(1, LIFE_HALO_RECV, left, LIFE_HALO_ROW, 0, ya, -xa, w + 2 * xa);
+        add(1, LIFE_HALO_RECV, right, LIFE_HALO_ROW, h + ya, ya, -xa, w + 2 * xa);
     }
     if (ops) {
         if (max_ops < n) return LIFE_EINVAL;

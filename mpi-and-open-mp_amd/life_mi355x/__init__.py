@@ -46,7 +46,7 @@ ABI_SYMBOLS = (
     "life_get_unique_id", "life_dev_create_rank", "life_dev_upload", "life_dev_fill_random",
     "life_dev_step", "life_dev_gather", "life_dev_live_count", "life_dev_sync",
     "life_dev_layout", "life_dev_world", "life_dev_set_timing", "life_dev_kernel_stats",
-    "life_tune", "life_dev_destroy",
+    "life_tune", "life_tune_temporal", "life_dev_destroy",
 )
 
 
@@ -61,17 +61,18 @@ class LifeError(RuntimeError):
 class HaloOp(ctypes.Structure):
     _fields_ = [("phase", ctypes.c_int32), ("kind", ctypes.c_int32), ("peer", ctypes.c_int32),
                 ("what", ctypes.c_int32), ("index", ctypes.c_int64), ("first", ctypes.c_int64),
-                ("count", ctypes.c_int64)]
+                ("count", ctypes.c_int64), ("width", ctypes.c_int64)]
 
     def as_tuple(self):
-        return (self.phase, self.kind, self.peer, self.what, self.index, self.first, self.count)
+        return (self.phase, self.kind, self.peer, self.what, self.index, self.first, self.count, self.width)
 
 
 class Layout(ctypes.Structure):
     _fields_ = [("w", ctypes.c_int64), ("h", ctypes.c_int64), ("x0", ctypes.c_int64),
                 ("y0", ctypes.c_int64), ("pitch", ctypes.c_int64), ("xoff", ctypes.c_int64),
-                ("rows", ctypes.c_int64), ("units", ctypes.c_int64), ("kernel", ctypes.c_int32),
-                ("coords", ctypes.c_int32 * 2)]
+                ("rows", ctypes.c_int64), ("units", ctypes.c_int64), ("xapron", ctypes.c_int64),
+                ("yapron", ctypes.c_int64), ("kernel", ctypes.c_int32), ("coords", ctypes.c_int32 * 2),
+                ("generations_per_exchange", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 _LIB = None
@@ -90,7 +91,7 @@ def _lib():
         L.life_decomposition.restype = None
         L.life_dims_create.argtypes = [i32, P(ctypes.c_int)]
         L.life_dims_create.restype = None
-        L.life_halo_plan.argtypes = [i64, i64, i32, i32, i32, P(HaloOp), i32]
+        L.life_halo_plan.argtypes = [i64, i64, i32, i32, i32, i32, P(HaloOp), i32]
         L.life_layout_query.argtypes = [i64, i64, i32, i32, i32, i32, P(Layout)]
         L.life_strerror.argtypes = [i32]
         L.life_strerror.restype = ctypes.c_char_p
@@ -111,6 +112,7 @@ def _lib():
         L.life_dev_set_timing.argtypes = [vp, i32]
         L.life_dev_kernel_stats.argtypes = [vp, P(ctypes.c_double), P(i64), P(ctypes.c_double)]
         L.life_tune.argtypes = [i32, i32, i32]
+        L.life_tune_temporal.argtypes = [i32]
         L.life_dev_destroy.argtypes = [vp]
         L.life_dev_destroy.restype = None
         _LIB = L
@@ -144,10 +146,11 @@ def dims_create(n: int):
     return d[0], d[1]
 
 
-def halo_plan(nx: int, ny: int, dims, rank: int):
-    """The per-generation halo ops of shard `rank` (see life_halo_plan)."""
+def halo_plan(nx: int, ny: int, dims, rank: int, kernel="byte"):
+    """The per-exchange halo ops of shard `rank` (see life_halo_plan)."""
     ops = (HaloOp * 16)()
-    n = _check(_lib().life_halo_plan(nx, ny, dims[0], dims[1], rank, ops, 16), "life_halo_plan")
+    n = _check(_lib().life_halo_plan(nx, ny, dims[0], dims[1], rank, kernel_id(kernel), ops, 16),
+               "life_halo_plan")
     return [ops[i].as_tuple() for i in range(n)]
 
 
@@ -160,6 +163,11 @@ def layout_query(nx: int, ny: int, dims, rank: int, kernel="byte") -> Layout:
 
 def density_to_thr(density: float) -> int:
     return min(int(density * 2.0**32), 0xFFFFFFFF)
+
+
+def tune_temporal(rows: int = 0) -> None:
+    """Temporal tile height (registers rows per lane: 48/64/80/96)."""
+    _check(_lib().life_tune_temporal(rows), "life_tune_temporal")
 
 
 def tune(rows: int = 0, depth: int = 0, kernel=-1) -> None:

@@ -23,7 +23,33 @@ p.add_argument("--rows", default="16,32,64")
 p.add_argument("--depths", default="2,4,8")
 p.add_argument("--gens", type=int, default=10)
 p.add_argument("--rounds", type=int, default=3)
+p.add_argument("--temporal", default="", help="bit temporal tile heights to A/B, e.g. 48,64,80,96")
 a = p.parse_args()
+
+if a.temporal:
+    heights = [int(v) for v in a.temporal.split(",")]
+    life = lm.Life(a.size, a.size, kernel="bit")
+    life.fill_random(1, 0.5)
+    res = {v: [] for v in heights}
+    for rnd in range(a.rounds):
+        for v in heights:
+            lm.tune_temporal(v)
+            life.step(8)
+            life.sync()
+            life.set_timing(True)
+            life.step(8 * a.gens)
+            ms, n, b = life.kernel_stats()
+            life.set_timing(False)
+            res[v].append((ms, b))
+    for v in heights:
+        mss = [m for m, _ in res[v]]
+        b = res[v][0][1]
+        med = statistics.median(mss)
+        print(json.dumps({"kernel": "bit-temporal", "rows": v, "median_ms_per_launch": round(med, 4),
+                          "gens_per_launch": 8, "Gcells_per_s": round(b / 0.25 / med / 1e6, 1),
+                          "alg_GBps": round(b / med / 1e6, 1)}), flush=True)
+    life.close()
+    sys.exit(0)
 
 variants = [(r, d) for r in map(int, a.rows.split(",")) for d in map(int, a.depths.split(","))]
 for kernel in a.kernels.split(","):

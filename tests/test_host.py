@@ -93,7 +93,7 @@ def test_layout_invariants(lm, kernel, nx, ny, dims):
         assert L.units == -(-L.w // cpu)
         assert L.pitch % 256 == 0 and L.xoff % 16 == 0
         assert L.pitch >= L.xoff + 16 * L.units + 16  # last unit, apron cell, right extra dword
-        assert L.rows == L.h + 2
+        assert L.rows == L.h + 2 * L.yapron
         assert (L.x0, L.x0 + L.w) == lm.decomposition(nx, dims[0], r // dims[1])
         assert (L.y0, L.y0 + L.h) == lm.decomposition(ny, dims[1], r % dims[1])
 
@@ -103,30 +103,46 @@ def test_layout_rejects_empty_blocks(lm):
         lm.layout_query(3, 10, (4, 1), 0)
 
 
+@pytest.mark.parametrize("kernel", ["byte", "bit"])
 @pytest.mark.parametrize("nx,ny,dims", [(10, 10, (2, 2)), (500, 500, (4, 2)), (7, 5, (2, 1)), (7, 5, (1, 2)),
-                                        (9, 9, (3, 3)), (5, 5, (1, 1)), (100, 3, (4, 3))])
-def test_halo_plan_is_symmetric(lm, nx, ny, dims):
-    """Every recv has a matching send at the peer: same phase, same size,
+                                        (9, 9, (3, 3)), (5, 5, (1, 1)), (100, 3, (4, 3)), (256, 64, (2, 2)),
+                                        (512, 80, (4, 2)), (64, 40, (1, 4)), (256, 9, (4, 1))])
+def test_halo_plan_is_symmetric(lm, kernel, nx, ny, dims):
+    """Every recv has a matching send at the peer: same phase, same shape,
     matched in issue order (RCCL p2p semantics), and sends go to the Cartesian
     neighbour whose apron they fill."""
     world = dims[0] * dims[1]
-    plans = {r: lm.halo_plan(nx, ny, dims, r) for r in range(world)}
-    lay = {r: lm.layout_query(nx, ny, dims, r) for r in range(world)}
+    plans = {r: lm.halo_plan(nx, ny, dims, r, kernel) for r in range(world)}
+    lay = {r: lm.layout_query(nx, ny, dims, r, kernel) for r in range(world)}
     for r, ops in plans.items():
+        xa, ya = lay[r].xapron, lay[r].yapron
         for phase in (0, 1):
             ph = [o for o in ops if o[0] == phase]
             if dims[phase] == 1:
                 assert [o[1] for o in ph] == [lm.HALO_FILL]
                 continue
             assert [o[1] for o in ph] == [lm.HALO_SEND, lm.HALO_SEND, lm.HALO_RECV, lm.HALO_RECV]
-            for k, o in enumerate(o for o in ph if o[1] == lm.HALO_RECV):
+            for o in (o for o in ph if o[1] == lm.HALO_RECV):
                 peer = o[2]
-                prev_from_peer = [q for q in ph if q[1] == lm.HALO_RECV and q[2] == peer]
-                kth = prev_from_peer.index(o)
-                sends = [q for q in plans[peer] if q[0] == phase and q[1] == lm.HALO_SEND and q[2] == r]
-                s = sends[kth]
-                assert s[6] == o[6]  # same cell count
-                if phase == 0:  # column: receiver x=-1 <- sender's last column
-                    assert (o[4], s[4]) in ((-1, lay[peer].w - 1), (lay[r].w, 0))
-                else:
-                    assert (o[4], s[4]) in ((0, lay[peer].h), (lay[r].h + 1, 1))
+                kth = [q for q in ph if q[1] == lm.HALO_RECV and q[2] == peer].index(o)
+                s_ = [q for q in plans[peer] if q[0] == phase and q[1] == lm.HALO_SEND and q[2] == r][kth]
+                assert (s_[6], s_[7]) == (o[6], o[7])  # same cells x rows
+                if phase == 0:  # x-apron <- the peer's edge columns
+                    assert o[7] == xa
+                    assert (o[4], s_[4]) in ((-xa, lay[peer].w - xa), (lay[r].w, 0))
+                else:  # y-apron rows <- the peer's edge rows (padded row = owned + yapron)
+                    assert o[7] == ya
+                    assert (o[4], s_[4]) in ((0, lay[peer].h), (lay[r].h + ya, ya))
+
+
+@pytest.mark.parametrize("nx,ny,dims,temporal", [(65536, 65536, (1, 1), True), (262144, 131072, (4, 2), True),
+                                                 (1000, 37, (1, 1), False), (64, 7, (2, 1), True),
+                                                 (64, 14, (1, 2), False), (96, 16, (3, 2), True)])
+def test_temporal_mode_selection(lm, nx, ny, dims, temporal):
+    for r in range(dims[0] * dims[1]):
+        L = lm.layout_query(nx, ny, dims, r, "bit")
+        assert (L.generations_per_exchange == 8) == temporal
+        assert (L.xapron, L.yapron) == ((32, 8) if temporal else (1, 1))
+        assert L.rows == L.h + 2 * L.yapron
+        B = lm.layout_query(nx, ny, dims, r, "byte")
+        assert (B.xapron, B.yapron, B.generations_per_exchange) == (1, 1, 1)
