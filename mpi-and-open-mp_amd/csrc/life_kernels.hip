@@ -315,12 +315,43 @@ struct TArgs {
     int32_t m;
 };
 
+// Neighbour words with bound_ctrl: lanes 0 / 63 read 0 (their outer bits are
+// allowed to be wrong), and the DPP move needs no `old` operand copy.
+__device__ __forceinline__ uint32_t left_or_zero(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xf, 0xf, true);
+}
+__device__ __forceinline__ uint32_t right_or_zero(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xf, 0xf, true);
+}
+
 __device__ __forceinline__ void bit_hsum(uint32_t v, uint32_t &s0, uint32_t &s1) {
-    const uint32_t L = __builtin_amdgcn_alignbit(v, from_left(0u, v), 31);
-    const uint32_t R = __builtin_amdgcn_alignbit(from_right(0u, v), v, 1);
+    const uint32_t L = __builtin_amdgcn_alignbit(v, left_or_zero(v), 31);
+    const uint32_t R = __builtin_amdgcn_alignbit(right_or_zero(v), v, 1);
     BitEnc::fa(L, v, R, s0, s1);
 }
 
+// One generation over register rows [lo, hi) (rows outside keep their old,
+// no longer needed values; a row outside [0, NR) counts as dead).
+template <int NR>
+__device__ __forceinline__ void tgen_rows(uint32_t (&v)[NR], const int lo, const int hi) {
+    uint32_t p0 = 0u, p1 = 0u, c0, c1;
+    if (lo > 0) bit_hsum(v[lo - 1], p0, p1);
+    bit_hsum(v[lo], c0, c1);
+#pragma unroll
+    for (int r = lo; r < hi; ++r) {
+        uint32_t n0 = 0u, n1 = 0u;
+        if (r + 1 < NR) bit_hsum(v[r + 1], n0, n1);
+        v[r] = BitEnc::rule1(p0, p1, c0, c1, n0, n1, v[r]);
+        p0 = c0;
+        p1 = c1;
+        c0 = n0;
+        c1 = n1;
+    }
+}
+
+// (A fully unrolled variant that skips the rows generation g no longer
+// needs -- ghost-zone shrink, 11-14 % fewer ops -- spilled at every
+// occupancy bound tried on ROCm 7.2 and was dropped)
 template <int NR, bool WRAPX, bool WRAPY>
 __global__ __launch_bounds__(kBlock) void tstep_kernel(TArgs a) {
     constexpr int T = NR - 2 * kTK;
@@ -354,20 +385,7 @@ __global__ __launch_bounds__(kBlock) void tstep_kernel(TArgs a) {
         ++y;
         if (WRAPY && y == a.h) y = 0;
     }
-    for (int g = 0; g < a.m; ++g) {
-        uint32_t p0 = 0u, p1 = 0u, c0, c1;  // row -1 of the tile counts as dead
-        bit_hsum(v[0], c0, c1);
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            uint32_t n0 = 0u, n1 = 0u;
-            if (r + 1 < NR) bit_hsum(v[r + 1], n0, n1);
-            v[r] = BitEnc::rule1(p0, p1, c0, c1, n0, n1, v[r]);
-            p0 = c0;
-            p1 = c1;
-            c0 = n0;
-            c1 = n1;
-        }
-    }
+    for (int g = 0; g < a.m; ++g) tgen_rows<NR>(v, 0, NR);
     const bool st = lane >= 1 && lane <= 62 && j < a.W;
     const int64_t yo = ty * T;  // owned row of register row K
     uint8_t *dst = a.out + (yo + a.ya) * a.pitch + voff;
@@ -541,8 +559,8 @@ namespace {
 // byte R64/D2 were the fastest of {16,32,64} x {2,4,8}.
 struct Tunings {
     StepTuning t[2];  // [0] byte, [1] bit
-    int nr = 80;      // temporal tile: registers rows per lane (T = nr - 2K); 80 and 96
-                      // tied fastest at 65536^2 (profiles/r01/tune_temporal.jsonl)
+    int nr = 96;      // temporal tile: registers rows per lane (T = nr - 2K); fastest of
+                      // 48/64/80/96 at 65536^2 (profiles/r01/tune_temporal.jsonl)
     Tunings() : t{{64, 2}, {16, 8}} {
         for (StepTuning &v : t) {
             if (const char *e = getenv("LIFE_STEP_ROWS")) v.rows = atoi(e);
@@ -561,7 +579,7 @@ StepTuning step_tuning(bool bit) { return tunings().t[bit ? 1 : 0]; }
 
 int temporal_rows() {
     const int nr = tunings().nr;
-    return nr == 48 || nr == 64 || nr == 96 ? nr : 80;
+    return nr == 48 || nr == 64 || nr == 80 ? nr : 96;
 }
 
 void set_temporal_rows(int nr) {
@@ -678,8 +696,8 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
     switch (temporal_rows()) {
     case 48: return launch_t<48>(a, wrap, grid, s);
     case 64: return launch_t<64>(a, wrap, grid, s);
-    case 96: return launch_t<96>(a, wrap, grid, s);
-    default: return launch_t<80>(a, wrap, grid, s);
+    case 80: return launch_t<80>(a, wrap, grid, s);
+    default: return launch_t<96>(a, wrap, grid, s);
     }
 }
 

@@ -134,4 +134,4 @@ def test_temporal_tile_heights_agree(gpu, oracle, rows):
             life.step(29)
             np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, 29, threads=4))
     finally:
-        gpu.tune_temporal(80)
+        gpu.tune_temporal(96)
