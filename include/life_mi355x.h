@@ -169,6 +169,15 @@ int life_dev_world(life_dev *d, int *world, int *dims0, int *dims1, int *nlocal,
  * algorithmic HBM bytes one launch moves (1 B read + 1 B written per cell for
  * BYTE, 2 bits for BIT, over the cells that launch updates). */
 int life_dev_set_timing(life_dev *d, int on);
+
+/* Execution-path switches (defaults 1): LIFE_OPT_SMALL_GRID lets a
+ * single-shard grid that fits one CU's LDS run all generations of a step call
+ * in one resident-workgroup launch; LIFE_OPT_OVERLAP overlaps the halo
+ * exchange with the interior kernel on partitioned grids.  Results are
+ * identical either way (tests switch them to reach every kernel). */
+#define LIFE_OPT_SMALL_GRID 1
+#define LIFE_OPT_OVERLAP 2
+int life_dev_configure(life_dev *d, int option, int value);
 int life_dev_kernel_stats(life_dev *d, double *avg_ms, int64_t *launches, double *bytes_per_launch);
 
 /* Stencil tuning for the whole process, per kernel family (-1: both): rows

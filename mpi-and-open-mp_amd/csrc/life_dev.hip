@@ -71,12 +71,14 @@ struct Shard {
     life_layout lay{};
     uint8_t *buf[2] = {nullptr, nullptr};
     int cur = 0;
-    hipStream_t stream = nullptr;  // compute
+    hipStream_t stream = nullptr;   // compute: whole-block kernels, boundary ring
+    hipStream_t stream2 = nullptr;  // compute: interior, concurrent with ring + halo
     hipStream_t comm_stream = nullptr;
-    hipEvent_t ev_ring = nullptr, ev_halo = nullptr, ev_sync = nullptr;
+    hipEvent_t ev_ring = nullptr, ev_halo = nullptr, ev_sync = nullptr, ev_int = nullptr, ev_join = nullptr;
     ncclComm_t comm = nullptr;
     uint8_t *col_send = nullptr, *col_recv = nullptr;  // 2*h bytes each
     unsigned long long *d_count = nullptr;
+    unsigned long long *h_count = nullptr;  // pinned
     uint8_t *sink = nullptr;  // stencil stores of lanes outside a region
     std::vector<life_halo_op> plan;
     std::vector<TimedLaunch> timers;
@@ -94,6 +96,7 @@ struct life_dev {
     bool rank_mode = false;
     bool timing = false;
     bool overlap = true;
+    bool small_ok = true;  // LDS-resident path for grids that fit one CU
     std::vector<Shard> shards;
     double acc_ms = 0.0;
     int64_t acc_launches = 0;
@@ -112,7 +115,10 @@ int shard_alloc(life_dev *d, Shard &s) {
         HIPCHK(hipMemset(s.buf[i], 0, bytes));
     }
     HIPCHK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&s.stream2, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&s.comm_stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&s.ev_int, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&s.ev_join, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&s.ev_ring, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&s.ev_halo, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&s.ev_sync, hipEventDisableTiming));
@@ -121,6 +127,7 @@ int shard_alloc(life_dev *d, Shard &s) {
     HIPCHK(hipMalloc(&s.col_recv, col_bytes));
     HIPCHK(hipMalloc(&s.d_count, sizeof(unsigned long long)));
     HIPCHK(hipMalloc(&s.sink, 1024));
+    HIPCHK(hipHostMalloc(&s.h_count, sizeof *s.h_count, hipHostMallocDefault));
     life_halo_op ops[16];
     const int n = life_halo_plan(d->nx, d->ny, d->dims[0], d->dims[1], s.rank, d->kernel, ops, 16);
     if (n < 0) {
@@ -141,9 +148,11 @@ void shard_free(Shard &s) {
     for (uint8_t *p : {s.buf[0], s.buf[1], s.col_send, s.col_recv, s.sink})
         if (p) (void)hipFree(p);
     if (s.d_count) (void)hipFree(s.d_count);
-    for (hipEvent_t e : {s.ev_ring, s.ev_halo, s.ev_sync})
+    if (s.h_count) (void)hipHostFree(s.h_count);
+    for (hipEvent_t e : {s.ev_ring, s.ev_halo, s.ev_sync, s.ev_int, s.ev_join})
         if (e) (void)hipEventDestroy(e);
     if (s.stream) (void)hipStreamDestroy(s.stream);
+    if (s.stream2) (void)hipStreamDestroy(s.stream2);
     if (s.comm_stream) (void)hipStreamDestroy(s.comm_stream);
 }
 
@@ -277,30 +286,41 @@ int exchange(life_dev *d, int which_rel, bool on_comm) {
     return LIFE_OK;
 }
 
-// Launches one stencil region; when timing is on and `timed`, brackets it
-// with HIP events on the shard's compute stream and books its algorithmic
-// bytes (1 B read + 1 B written per BYTE cell, 2 bits per BIT cell).
-int launch_region(life_dev *d, Shard &s, const life::Region &r, bool timed) {
-    const uint8_t *in = s.buf[s.cur];
-    uint8_t *out = s.buf[s.cur ^ 1];
-    if (!d->timing || !timed) {
-        HIPCHK(life::launch_step(s.lay, in, out, s.sink, r, wrap_of(d), s.stream));
-        return LIFE_OK;
-    }
+TimedLaunch *timer_slot(Shard &s, int *rc) {
+    *rc = LIFE_OK;
     if (s.timers_used == s.timers.size()) {
         TimedLaunch t;
-        HIPCHK(hipEventCreate(&t.a));
-        HIPCHK(hipEventCreate(&t.b));
+        if (hipEventCreate(&t.a) != hipSuccess || hipEventCreate(&t.b) != hipSuccess) {
+            set_err("hipEventCreate failed");
+            *rc = LIFE_EHIP;
+            return nullptr;
+        }
         s.timers.push_back(t);
     }
-    TimedLaunch &t = s.timers[s.timers_used++];
-    HIPCHK(hipEventRecord(t.a, s.stream));
-    HIPCHK(life::launch_step(s.lay, in, out, s.sink, r, wrap_of(d), s.stream));
-    HIPCHK(hipEventRecord(t.b, s.stream));
-    const bool bit = s.lay.kernel == LIFE_KERNEL_BIT;
-    const int64_t cpu = bit ? 128 : 16;
-    const int64_t xa = r.u0 * cpu, xb = r.u1 * cpu < s.lay.w ? r.u1 * cpu : s.lay.w;
-    d->acc_bytes += (double)(xb - xa) * (double)(r.r1 - r.r0) * (bit ? 0.25 : 2.0);
+    return &s.timers[s.timers_used++];
+}
+
+// Launches one stencil region on `st`; when timing is on and `timed`,
+// brackets it with HIP events on that stream and books its algorithmic bytes
+// (1 B read + 1 B written per BYTE cell, 2 bits per BIT cell).
+int launch_region(life_dev *d, Shard &s, const life::Region &r, bool timed, hipStream_t st) {
+    const uint8_t *in = s.buf[s.cur];
+    uint8_t *out = s.buf[s.cur ^ 1];
+    TimedLaunch *t = nullptr;
+    if (d->timing && timed) {
+        int rc;
+        t = timer_slot(s, &rc);
+        if (!t) return rc;
+        HIPCHK(hipEventRecord(t->a, st));
+    }
+    HIPCHK(life::launch_step(s.lay, in, out, s.sink, r, wrap_of(d), st));
+    if (t) {
+        HIPCHK(hipEventRecord(t->b, st));
+        const bool bit = s.lay.kernel == LIFE_KERNEL_BIT;
+        const int64_t cpu = bit ? 128 : 16;
+        const int64_t xa = r.u0 * cpu, xb = r.u1 * cpu < s.lay.w ? r.u1 * cpu : s.lay.w;
+        d->acc_bytes += (double)(xb - xa) * (double)(r.r1 - r.r0) * (bit ? 0.25 : 2.0);
+    }
     return LIFE_OK;
 }
 
@@ -321,44 +341,57 @@ int harvest_timers(life_dev *d) {
 
 bool temporal(const life_dev *d) { return d->shards[0].lay.generations_per_exchange > 1; }
 
-// Launches one tile region of the temporal stencil (m generations, cur -> nxt).
-int launch_tiles(life_dev *d, Shard &s, const life::TileRegion &r, int m, bool timed) {
+// Launches up to 4 tile regions of the temporal stencil as ONE kernel on
+// `st` (m generations, cur -> nxt), optionally timed.
+int launch_tiles(life_dev *d, Shard &s, const life::TileRegion *r, int nreg, int m, bool timed, hipStream_t st) {
     const uint8_t *in = s.buf[s.cur];
     uint8_t *out = s.buf[s.cur ^ 1];
     TimedLaunch *t = nullptr;
     if (d->timing && timed) {
-        if (s.timers_used == s.timers.size()) {
-            TimedLaunch n;
-            HIPCHK(hipEventCreate(&n.a));
-            HIPCHK(hipEventCreate(&n.b));
-            s.timers.push_back(n);
-        }
-        t = &s.timers[s.timers_used++];
-        HIPCHK(hipEventRecord(t->a, s.stream));
+        int rc;
+        t = timer_slot(s, &rc);
+        if (!t) return rc;
+        HIPCHK(hipEventRecord(t->a, st));
     }
-    HIPCHK(life::launch_tstep(s.lay, in, out, r, m, wrap_of(d), s.stream));
+    HIPCHK(life::launch_tstep(s.lay, in, out, r, nreg, m, wrap_of(d), st));
     if (t) {
-        HIPCHK(hipEventRecord(t->b, s.stream));
+        HIPCHK(hipEventRecord(t->b, st));
         const life::TileGeom g = life::tile_geom(s.lay);
         const int64_t W = s.lay.w / 32;
-        const int64_t wa = r.tx0 * g.words, wb = r.tx1 * g.words < W ? r.tx1 * g.words : W;
-        const int64_t ya = r.ty0 * g.rows, yb = r.ty1 * g.rows < s.lay.h ? r.ty1 * g.rows : s.lay.h;
-        // algorithmic bytes of the cell-updates this launch performs (0.25 B each)
-        d->acc_bytes += (double)(wb - wa) * 32.0 * (double)(yb - ya) * (double)m * 0.25;
+        for (int k = 0; k < nreg; k++) {
+            const int64_t wa = r[k].tx0 * g.words, wb = r[k].tx1 * g.words < W ? r[k].tx1 * g.words : W;
+            const int64_t ya = r[k].ty0 * g.rows, yb = r[k].ty1 * g.rows < s.lay.h ? r[k].ty1 * g.rows : s.lay.h;
+            if (wb > wa && yb > ya)  // algorithmic bytes of the cell-updates performed (0.25 B each)
+                d->acc_bytes += (double)(wb - wa) * 32.0 * (double)(yb - ya) * (double)m * 0.25;
+        }
     }
     return LIFE_OK;
 }
 
+// Block boundary of the overlapped schedule: both compute streams wait for
+// the interior (stream2), the ring (stream) and the halo (comm stream).
+int join_streams(Shard &s) {
+    HIPCHK(hipEventRecord(s.ev_int, s.stream2));
+    HIPCHK(hipStreamWaitEvent(s.stream, s.ev_int, 0));
+    HIPCHK(hipStreamWaitEvent(s.stream, s.ev_halo, 0));
+    HIPCHK(hipEventRecord(s.ev_join, s.stream));
+    HIPCHK(hipStreamWaitEvent(s.stream2, s.ev_join, 0));
+    return LIFE_OK;
+}
+
 // m <= K generations of the temporally blocked bit stencil on every shard,
-// then one K-deep halo exchange (the ring tiles first, the exchange of the
-// new state on the comm stream overlapped with the interior tiles).
+// then one K-deep halo exchange.  Partitioned shards: the boundary ring tiles
+// (one multi-region launch) run on the compute stream, the exchange of their
+// new state on the comm stream, and the interior tiles concurrently on the
+// second compute stream.
 int generation_block(life_dev *d, int m) {
     const bool rx = d->dims[0] > 1, ry = d->dims[1] > 1;
     if (!(rx || ry)) {
         for (Shard &s : d->shards) {
             HIPCHK(hipSetDevice(s.device));
             const life::TileGeom g = life::tile_geom(s.lay);
-            CHK(launch_tiles(d, s, life::TileRegion{0, g.ntx, 0, g.nty}, m, true));
+            const life::TileRegion all{0, g.ntx, 0, g.nty};
+            CHK(launch_tiles(d, s, &all, 1, m, true, s.stream));
         }
         for (Shard &s : d->shards) s.cur ^= 1;
         return LIFE_OK;
@@ -368,70 +401,69 @@ int generation_block(life_dev *d, int m) {
         const life::TileGeom g = life::tile_geom(s.lay);
         const int64_t TX = g.ntx, TY = g.nty;
         const int64_t ra = ry ? 1 : 0, rb = ry ? TY - 1 : TY;
+        life::TileRegion ring[4];
+        int n = 0;
         if (ry) {
-            CHK(launch_tiles(d, s, life::TileRegion{0, TX, 0, 1}, m, false));
-            if (TY > 1) CHK(launch_tiles(d, s, life::TileRegion{0, TX, TY - 1, TY}, m, false));
+            ring[n++] = life::TileRegion{0, TX, 0, 1};
+            if (TY > 1) ring[n++] = life::TileRegion{0, TX, TY - 1, TY};
         }
         if (rx && rb > ra) {
-            CHK(launch_tiles(d, s, life::TileRegion{0, 1, ra, rb}, m, false));
-            if (TX > 1) CHK(launch_tiles(d, s, life::TileRegion{TX - 1, TX, ra, rb}, m, false));
+            ring[n++] = life::TileRegion{0, 1, ra, rb};
+            if (TX > 1) ring[n++] = life::TileRegion{TX - 1, TX, ra, rb};
         }
+        CHK(launch_tiles(d, s, ring, n, m, false, s.stream));
         HIPCHK(hipEventRecord(s.ev_ring, s.stream));
         HIPCHK(hipStreamWaitEvent(s.comm_stream, s.ev_ring, 0));
+        const int64_t ua = rx ? 1 : 0, ub = rx ? TX - 1 : TX;
+        const life::TileRegion inner{ua, ub, ra, rb};
+        if (rb > ra && ub > ua) CHK(launch_tiles(d, s, &inner, 1, m, true, s.stream2));
     }
     CHK(exchange(d, 1, true));
     for (Shard &s : d->shards) {
         HIPCHK(hipSetDevice(s.device));
-        const life::TileGeom g = life::tile_geom(s.lay);
-        const int64_t TX = g.ntx, TY = g.nty;
-        const int64_t ra = ry ? 1 : 0, rb = ry ? TY - 1 : TY;
-        const int64_t ua = rx ? 1 : 0, ub = rx ? TX - 1 : TX;
-        if (rb > ra && ub > ua) CHK(launch_tiles(d, s, life::TileRegion{ua, ub, ra, rb}, m, true));
         HIPCHK(hipEventRecord(s.ev_halo, s.comm_stream));
-        HIPCHK(hipStreamWaitEvent(s.stream, s.ev_halo, 0));
+        CHK(join_streams(s));
     }
     for (Shard &s : d->shards) s.cur ^= 1;
     return LIFE_OK;
 }
 
-// One generation on every local shard.
+// One generation on every local shard (one-cell aprons).
 int generation(life_dev *d) {
     const bool rx = d->dims[0] > 1, ry = d->dims[1] > 1;
     if (!d->overlap || !(rx || ry)) {
         for (Shard &s : d->shards) {
             HIPCHK(hipSetDevice(s.device));
-            CHK(launch_region(d, s, life::Region{0, s.lay.units, 0, s.lay.h}, true));
+            CHK(launch_region(d, s, life::Region{0, s.lay.units, 0, s.lay.h}, true, s.stream));
         }
         for (Shard &s : d->shards) s.cur ^= 1;
         return exchange(d, 0, false);
     }
     // Ring first (cells whose 3x3 neighbourhood reaches a partitioned axis'
-    // apron), then the halo of the new state on the comm stream, overlapped
-    // with the interior on the compute stream.
+    // apron) on the compute stream, then the halo of the new state on the
+    // comm stream; the interior runs concurrently on the second compute stream.
     for (Shard &s : d->shards) {
         HIPCHK(hipSetDevice(s.device));
         const int64_t U = s.lay.units, H = s.lay.h;
         const int64_t ra = ry ? 1 : 0, rb = ry ? H - 1 : H;  // interior rows
         if (ry) {
-            CHK(launch_region(d, s, life::Region{0, U, 0, 1}, false));
-            if (H > 1) CHK(launch_region(d, s, life::Region{0, U, H - 1, H}, false));
+            CHK(launch_region(d, s, life::Region{0, U, 0, 1}, false, s.stream));
+            if (H > 1) CHK(launch_region(d, s, life::Region{0, U, H - 1, H}, false, s.stream));
         }
         if (rx && rb > ra) {
-            CHK(launch_region(d, s, life::Region{0, 1, ra, rb}, false));
-            if (U > 1) CHK(launch_region(d, s, life::Region{U - 1, U, ra, rb}, false));
+            CHK(launch_region(d, s, life::Region{0, 1, ra, rb}, false, s.stream));
+            if (U > 1) CHK(launch_region(d, s, life::Region{U - 1, U, ra, rb}, false, s.stream));
         }
         HIPCHK(hipEventRecord(s.ev_ring, s.stream));
         HIPCHK(hipStreamWaitEvent(s.comm_stream, s.ev_ring, 0));
+        const int64_t ua = rx ? 1 : 0, ub = rx ? U - 1 : U;
+        if (rb > ra && ub > ua) CHK(launch_region(d, s, life::Region{ua, ub, ra, rb}, true, s.stream2));
     }
     CHK(exchange(d, 1, true));  // halo of nxt on the comm streams
     for (Shard &s : d->shards) {
         HIPCHK(hipSetDevice(s.device));
-        const int64_t U = s.lay.units, H = s.lay.h;
-        const int64_t ra = ry ? 1 : 0, rb = ry ? H - 1 : H;
-        const int64_t ua = rx ? 1 : 0, ub = rx ? U - 1 : U;
-        if (rb > ra && ub > ua) CHK(launch_region(d, s, life::Region{ua, ub, ra, rb}, true));
         HIPCHK(hipEventRecord(s.ev_halo, s.comm_stream));
-        HIPCHK(hipStreamWaitEvent(s.stream, s.ev_halo, 0));
+        CHK(join_streams(s));
     }
     for (Shard &s : d->shards) s.cur ^= 1;
     return LIFE_OK;
@@ -584,8 +616,11 @@ int life_dev_upload(life_dev *d, const uint8_t *grid) {
         HIPCHK(hipSetDevice(s.device));
         uint8_t *stage = nullptr;
         HIPCHK(hipMalloc(&stage, (size_t)(L.w * L.h)));
-        HIPCHK(hipMemcpy2DAsync(stage, (size_t)L.w, grid + L.y0 * d->nx + L.x0, (size_t)d->nx, (size_t)L.w,
-                                (size_t)L.h, hipMemcpyHostToDevice, s.stream));
+        // Host buffers are the caller's pageable memory: blocking copies only
+        // (an async copy from/to pageable memory is staged by the runtime and
+        // was seen to race with the caller reading the buffer).
+        HIPCHK(hipMemcpy2D(stage, (size_t)L.w, grid + L.y0 * d->nx + L.x0, (size_t)d->nx, (size_t)L.w,
+                           (size_t)L.h, hipMemcpyHostToDevice));
         HIPCHK(life::launch_import_block(L, stage, s.buf[s.cur], s.stream));
         HIPCHK(hipStreamSynchronize(s.stream));
         HIPCHK(hipFree(stage));
@@ -608,8 +643,42 @@ int life_dev_fill_random(life_dev *d, uint64_t seed, uint32_t thr32) {
     return LIFE_OK;
 }
 
+// A single-shard grid small enough for one CU's LDS runs every generation of
+// the call in one resident-workgroup launch (life_kernels.hip, small_kernel).
+static bool small_grid(const life_dev *d) {
+    return d->world == 1 && d->shards.size() == 1 && d->small_ok &&
+           life::small_lds_bytes(d->shards[0].lay) <= life::kSmallMaxLds;
+}
+
+static int step_small(life_dev *d, int64_t generations) {
+    Shard &s = d->shards[0];
+    HIPCHK(hipSetDevice(s.device));
+    TimedLaunch *t = nullptr;
+    if (d->timing) {
+        int rc;
+        t = timer_slot(s, &rc);
+        if (!t) return rc;
+        HIPCHK(hipEventRecord(t->a, s.stream));
+    }
+    HIPCHK(life::launch_small(s.lay, s.buf[s.cur], s.buf[s.cur ^ 1], generations, s.stream));
+    if (t) {
+        HIPCHK(hipEventRecord(t->b, s.stream));
+        d->acc_bytes += (double)s.lay.w * (double)s.lay.h * (double)generations *
+                        (s.lay.kernel == LIFE_KERNEL_BIT ? 0.25 : 2.0);
+    }
+    s.cur ^= 1;
+    return LIFE_OK;
+}
+
 int life_dev_step(life_dev *d, int64_t generations) {
     if (!d || generations < 0) return LIFE_EINVAL;
+    if (generations == 0) return LIFE_OK;
+    if (small_grid(d)) {
+        constexpr int64_t kChunk = 1 << 20;  // generations per resident launch
+        for (int64_t g = 0; g < generations; g += kChunk)
+            CHK(step_small(d, generations - g < kChunk ? generations - g : kChunk));
+        return LIFE_OK;
+    }
     if (temporal(d)) {
         const int K = d->shards[0].lay.generations_per_exchange;
         for (int64_t g = 0; g < generations; g += K)
@@ -625,6 +694,7 @@ int life_dev_sync(life_dev *d) {
     for (Shard &s : d->shards) {
         HIPCHK(hipSetDevice(s.device));
         HIPCHK(hipStreamSynchronize(s.stream));
+        HIPCHK(hipStreamSynchronize(s.stream2));
         HIPCHK(hipStreamSynchronize(s.comm_stream));
     }
     return LIFE_OK;
@@ -645,9 +715,9 @@ int life_dev_gather(life_dev *d, uint8_t *grid) {
             uint8_t *stage = nullptr;
             HIPCHK(hipMalloc(&stage, (size_t)(L.w * L.h)));
             HIPCHK(life::launch_export_block(L, s.buf[s.cur], stage, s.stream));
-            HIPCHK(hipMemcpy2DAsync(grid + L.y0 * d->nx + L.x0, (size_t)d->nx, stage, (size_t)L.w, (size_t)L.w,
-                                    (size_t)L.h, hipMemcpyDeviceToHost, s.stream));
             HIPCHK(hipStreamSynchronize(s.stream));
+            HIPCHK(hipMemcpy2D(grid + L.y0 * d->nx + L.x0, (size_t)d->nx, stage, (size_t)L.w, (size_t)L.w,
+                               (size_t)L.h, hipMemcpyDeviceToHost));  // blocking: pageable destination
             HIPCHK(hipFree(stage));
         }
         return LIFE_OK;
@@ -668,17 +738,18 @@ int life_dev_gather(life_dev *d, uint8_t *grid) {
     if (s.rank != root) {
         NCCLCHK(ncclSend(stage, (size_t)(s.lay.w * s.lay.h), ncclUint8, root, s.comm, s.stream));
     } else {
-        HIPCHK(hipMemcpy2DAsync(grid + s.lay.y0 * d->nx + s.lay.x0, (size_t)d->nx, stage, (size_t)s.lay.w,
-                                (size_t)s.lay.w, (size_t)s.lay.h, hipMemcpyDeviceToHost, s.stream));
+        HIPCHK(hipStreamSynchronize(s.stream));
+        HIPCHK(hipMemcpy2D(grid + s.lay.y0 * d->nx + s.lay.x0, (size_t)d->nx, stage, (size_t)s.lay.w,
+                           (size_t)s.lay.w, (size_t)s.lay.h, hipMemcpyDeviceToHost));
         HIPCHK(hipMalloc(&rstage, (size_t)maxb));
         for (int r = 0; r < d->world && rc == LIFE_OK; r++) {
             if (r == root) continue;
             life_layout L;
             CHK(life_layout_query(d->nx, d->ny, d->dims[0], d->dims[1], r, d->kernel, &L));
             NCCLCHK(ncclRecv(rstage, (size_t)(L.w * L.h), ncclUint8, r, s.comm, s.stream));
-            HIPCHK(hipMemcpy2DAsync(grid + L.y0 * d->nx + L.x0, (size_t)d->nx, rstage, (size_t)L.w, (size_t)L.w,
-                                    (size_t)L.h, hipMemcpyDeviceToHost, s.stream));
             HIPCHK(hipStreamSynchronize(s.stream));
+            HIPCHK(hipMemcpy2D(grid + L.y0 * d->nx + L.x0, (size_t)d->nx, rstage, (size_t)L.w, (size_t)L.w,
+                               (size_t)L.h, hipMemcpyDeviceToHost));
         }
     }
     HIPCHK(hipStreamSynchronize(s.stream));
@@ -696,10 +767,9 @@ int64_t life_dev_live_count(life_dev *d) {
         HIPCHK(life::launch_live_count(s.lay, s.buf[s.cur], s.d_count, s.stream));
         if (d->rank_mode && d->world > 1)
             NCCLCHK(ncclAllReduce(s.d_count, s.d_count, 1, ncclUint64, ncclSum, s.comm, s.stream));
-        unsigned long long c = 0;
-        HIPCHK(hipMemcpyAsync(&c, s.d_count, sizeof c, hipMemcpyDeviceToHost, s.stream));
-        HIPCHK(hipStreamSynchronize(s.stream));
-        total += (int64_t)c;
+        HIPCHK(hipMemcpyAsync(s.h_count, s.d_count, sizeof *s.h_count, hipMemcpyDeviceToHost, s.stream));
+        HIPCHK(hipStreamSynchronize(s.stream));  // pinned destination
+        total += (int64_t)*s.h_count;
     }
     return total;
 }
@@ -718,6 +788,16 @@ int life_dev_world(life_dev *d, int *world, int *dims0, int *dims1, int *nlocal,
     if (nlocal) *nlocal = (int)d->shards.size();
     if (transport) *transport = d->transport;
     return LIFE_OK;
+}
+
+int life_dev_configure(life_dev *d, int option, int value) {
+    if (!d) return LIFE_EINVAL;
+    CHK(life_dev_sync(d));
+    switch (option) {
+    case LIFE_OPT_SMALL_GRID: d->small_ok = value != 0; return LIFE_OK;
+    case LIFE_OPT_OVERLAP: d->overlap = value != 0; return LIFE_OK;
+    default: return LIFE_EINVAL;
+    }
 }
 
 int life_dev_set_timing(life_dev *d, int on) {
@@ -759,6 +839,7 @@ void life_dev_destroy(life_dev *d) {
     for (Shard &s : d->shards) {
         (void)hipSetDevice(s.device);
         if (s.stream) (void)hipStreamSynchronize(s.stream);
+        if (s.stream2) (void)hipStreamSynchronize(s.stream2);
         if (s.comm_stream) (void)hipStreamSynchronize(s.comm_stream);
     }
     for (Shard &s : d->shards) shard_free(s);

@@ -56,10 +56,18 @@ struct TileGeom {
     int64_t words, rows, ntx, nty;
 };
 TileGeom tile_geom(const life_layout &L);
-hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, const TileRegion &r, int m,
-                        Wrap wrap, hipStream_t s);
+// Up to 4 disjoint tile regions in one launch.
+hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, const TileRegion *r, int nreg,
+                        int m, Wrap wrap, hipStream_t s);
 int temporal_rows();              // registers rows per lane (48/64/80/96)
 void set_temporal_rows(int nr);
+
+// LDS-resident path for small single-shard grids: all `gens` generations in
+// one single-workgroup launch (in -> out; in may equal out).  Usable when
+// small_lds_bytes(L) <= kSmallMaxLds.
+constexpr int64_t kSmallMaxLds = 160 * 1024;
+int64_t small_lds_bytes(const life_layout &L);
+hipError_t launch_small(const life_layout &L, const uint8_t *in, uint8_t *out, int64_t gens, hipStream_t s);
 
 // Column halo staging: pack writes the last xapron columns to slot 0 and the
 // first xapron columns to slot 1 (h rows each: 1 byte 0/1 per row for a cell

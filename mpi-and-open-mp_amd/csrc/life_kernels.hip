@@ -23,6 +23,7 @@
 //    the rule).
 #include "life_kernels.h"
 
+#include <stdint.h>
 #include <stdlib.h>
 
 namespace life {
@@ -307,12 +308,15 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs a) {
 // per 62 columns, instead of 2 x m full passes.
 constexpr int kTK = LIFE_TEMPORAL_DEPTH;
 
+constexpr int kMaxRegions = 4;
 struct TArgs {
     const uint8_t *in;
     uint8_t *out;
     int64_t pitch, xoff, W, h, ya;  // W = 32-bit words per owned row
-    int64_t tx0, tx1, ty0, ty1;     // tile region
-    int32_t m;
+    // up to kMaxRegions tile regions in one launch (the boundary ring of a
+    // partitioned shard); wave w belongs to the region with first[k] <= w
+    int64_t tx0[kMaxRegions], tx1[kMaxRegions], ty0[kMaxRegions], first[kMaxRegions + 1];
+    int32_t nreg, m;
 };
 
 // Neighbour words with bound_ctrl: lanes 0 / 63 read 0 (their outer bits are
@@ -358,9 +362,11 @@ __global__ __launch_bounds__(kBlock) void tstep_kernel(TArgs a) {
     const int lane = threadIdx.x & 63;
     // wave index: uniform, so every row address below is scalar (SALU) math
     const int64_t wv = (int64_t)blockIdx.x * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t ntx = a.tx1 - a.tx0;
-    const int64_t tx = a.tx0 + wv % ntx, ty = a.ty0 + wv / ntx;
-    if (ty >= a.ty1) return;  // whole wave
+    if (wv >= a.first[a.nreg]) return;  // whole wave
+    int k = 0;
+    while (k + 1 < a.nreg && wv >= a.first[k + 1]) ++k;
+    const int64_t ntx = a.tx1[k] - a.tx0[k], wr = wv - a.first[k];
+    const int64_t tx = a.tx0[k] + wr % ntx, ty = a.ty0[k] + wr / ntx;
     const int64_t j = tx * 62 + lane - 1;  // word column of this lane
     int64_t jl;
     if (WRAPX) {
@@ -397,6 +403,101 @@ __global__ __launch_bounds__(kBlock) void tstep_kernel(TArgs a) {
 #pragma unroll
         for (int r = 0; r < T; ++r)
             if (st && yo + r < a.h) *reinterpret_cast<uint32_t *>(dst + r * a.pitch) = v[kTK + r];
+    }
+}
+
+// ------------------------------------------------------------------ small grids
+// LDS-resident stencil for a grid that fits one CU (configs[1]: p46gun_big,
+// 500^2): one 1024-thread workgroup imports the shard into LDS as bits
+// (W = ceil(w/32) words per row, two h x W buffers), runs G generations with
+// one barrier each, and exports the result in the shard's own encoding.  No
+// HBM traffic and no launch per generation: the per-generation cost is
+// ~1-2k cycles of one CU instead of a full-chip launch.  Both axes wrap
+// inside the shard (single-shard grids only); a width that is not a
+// multiple of 32 is wrapped by the same patching as WRAPX.
+constexpr int kSmallThreads = 1024;
+
+struct SArgs {
+    const uint8_t *in;
+    uint8_t *out;
+    int64_t pitch, xoff, ya;
+    int32_t w, h, W, gens, bit;
+};
+
+__global__ __launch_bounds__(kSmallThreads) void small_kernel(SArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int W = a.W, h = a.h, w = a.w, n = W * h;
+    uint32_t *A = lds, *B = lds + n;
+    const int t = threadIdx.x;
+    const int q = w - 32 * (W - 1);                   // valid bits in the last word: 1..32
+    const uint32_t lastmask = q == 32 ? 0xFFFFFFFFu : ((1u << q) - 1u);
+    // import: one word per thread-iteration
+    for (int i = t; i < n; i += kSmallThreads) {
+        const int y = i / W, j = i % W;
+        const uint8_t *row = a.in + (int64_t)(y + a.ya) * a.pitch + a.xoff;
+        uint32_t v = 0;
+        if (a.bit) {
+            v = reinterpret_cast<const uint32_t *>(row)[j];
+        } else {
+            for (int k = 0; k < 32 && 32 * j + k < w; ++k) v |= (uint32_t)(row[32 * j + k] != 0) << k;
+        }
+        A[i] = j == W - 1 ? v & lastmask : v;
+    }
+    __syncthreads();
+    // thread -> (word column j, rows [y0, y1))
+    const int groups = kSmallThreads / W;  // W <= 1024 is checked on the host
+    const int j = t % W, g = t / W;
+    const int R = (h + groups - 1) / groups;
+    const int y0 = g < groups ? g * R : h, y1 = min(h, y0 + R);
+    const int jl = j == 0 ? W - 1 : j - 1, jr = j == W - 1 ? 0 : j + 1;
+    const uint32_t lshift = j == 0 ? 31u - (uint32_t)((w - 1) & 31) : 0u;  // bit of cell w-1 -> bit 31
+    const bool last = j == W - 1;
+    for (int gen = 0; gen < a.gens; ++gen) {
+        if (y0 < y1) {
+            auto hsum = [&](int y, uint32_t &s0, uint32_t &s1, uint32_t &c) {
+                y = y < 0 ? y + h : (y >= h ? y - h : y);
+                const uint32_t *r = A + y * W;
+                c = r[j];
+                uint32_t lw = r[jl] << lshift;
+                uint32_t rw = r[jr];
+                uint32_t cc = c;
+                if (last) {  // the cell right of w-1 is cell 0
+                    if (q < 32)
+                        cc = (cc & lastmask) | ((rw & 1u) << q);
+                }
+                const uint32_t L = __builtin_amdgcn_alignbit(cc, lw, 31);
+                const uint32_t Rr = __builtin_amdgcn_alignbit(rw, cc, 1);
+                BitEnc::fa(L, cc, Rr, s0, s1);
+            };
+            uint32_t p0, p1, c0, c1, n0, n1, cp, cc, cn;
+            hsum(y0 - 1, p0, p1, cp);
+            hsum(y0, c0, c1, cc);
+            for (int y = y0; y < y1; ++y) {
+                hsum(y + 1, n0, n1, cn);
+                const uint32_t v = BitEnc::rule1(p0, p1, c0, c1, n0, n1, cc);
+                B[y * W + j] = last ? v & lastmask : v;
+                p0 = c0;
+                p1 = c1;
+                c0 = n0;
+                c1 = n1;
+                cc = cn;
+            }
+        }
+        __syncthreads();
+        uint32_t *tmp = A;
+        A = B;
+        B = tmp;
+    }
+    // export into the shard's encoding (owned cells only)
+    for (int i = t; i < n; i += kSmallThreads) {
+        const int y = i / W, jj = i % W;
+        uint8_t *row = a.out + (int64_t)(y + a.ya) * a.pitch + a.xoff;
+        const uint32_t v = A[i];
+        if (a.bit) {
+            reinterpret_cast<uint32_t *>(row)[jj] = v;
+        } else {
+            for (int k = 0; k < 32 && 32 * jj + k < w; ++k) row[32 * jj + k] = (uint8_t)((v >> k) & 1u);
+        }
     }
 }
 
@@ -674,10 +775,9 @@ TileGeom tile_geom(const life_layout &L) {
     return g;
 }
 
-hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, const TileRegion &r, int m,
-                        Wrap wrap, hipStream_t s) {
-    if (r.tx1 <= r.tx0 || r.ty1 <= r.ty0 || m <= 0) return hipSuccess;
-    if (m > kTK || L.generations_per_exchange != kTK) return hipErrorInvalidValue;
+hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, const TileRegion *r, int nreg,
+                        int m, Wrap wrap, hipStream_t s) {
+    if (nreg < 0 || nreg > kMaxRegions || m > kTK || L.generations_per_exchange != kTK) return hipErrorInvalidValue;
     TArgs a;
     a.in = in;
     a.out = out;
@@ -686,12 +786,19 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
     a.W = L.w / 32;
     a.h = L.h;
     a.ya = L.yapron;
-    a.tx0 = r.tx0;
-    a.tx1 = r.tx1;
-    a.ty0 = r.ty0;
-    a.ty1 = r.ty1;
     a.m = m;
-    const int64_t waves = (r.tx1 - r.tx0) * (r.ty1 - r.ty0);
+    a.nreg = 0;
+    a.first[0] = 0;
+    for (int k = 0; k < nreg; k++) {
+        if (r[k].tx1 <= r[k].tx0 || r[k].ty1 <= r[k].ty0) continue;
+        const int n = a.nreg++;
+        a.tx0[n] = r[k].tx0;
+        a.tx1[n] = r[k].tx1;
+        a.ty0[n] = r[k].ty0;
+        a.first[n + 1] = a.first[n] + (r[k].tx1 - r[k].tx0) * (r[k].ty1 - r[k].ty0);
+    }
+    if (a.nreg == 0 || m <= 0) return hipSuccess;
+    const int64_t waves = a.first[a.nreg];
     const unsigned grid = (unsigned)((waves + kBlock / 64 - 1) / (kBlock / 64));
     switch (temporal_rows()) {
     case 48: return launch_t<48>(a, wrap, grid, s);
@@ -699,6 +806,36 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
     case 80: return launch_t<80>(a, wrap, grid, s);
     default: return launch_t<96>(a, wrap, grid, s);
     }
+}
+
+int64_t small_lds_bytes(const life_layout &L) {
+    const int64_t W = (L.w + 31) / 32;
+    return W > kSmallThreads ? INT64_MAX : 2 * W * L.h * 4;
+}
+
+hipError_t launch_small(const life_layout &L, const uint8_t *in, uint8_t *out, int64_t gens, hipStream_t s) {
+    const int64_t bytes = small_lds_bytes(L);
+    if (bytes > kSmallMaxLds || gens <= 0 || gens > INT32_MAX) return hipErrorInvalidValue;
+    static bool attr_set = false;  // opt in to more than 64 KiB of dynamic LDS
+    if (!attr_set) {
+        const hipError_t e = hipFuncSetAttribute((const void *)small_kernel,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSmallMaxLds);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    SArgs a;
+    a.in = in;
+    a.out = out;
+    a.pitch = L.pitch;
+    a.xoff = L.xoff;
+    a.ya = L.yapron;
+    a.w = (int32_t)L.w;
+    a.h = (int32_t)L.h;
+    a.W = (int32_t)((L.w + 31) / 32);
+    a.gens = (int32_t)gens;
+    a.bit = is_bit(L) ? 1 : 0;
+    small_kernel<<<1, kSmallThreads, (size_t)bytes, s>>>(a);
+    return hipGetLastError();
 }
 
 hipError_t launch_pack_columns(const life_layout &L, const uint8_t *buf, uint8_t *stage, hipStream_t s) {

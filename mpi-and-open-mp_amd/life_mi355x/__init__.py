@@ -38,6 +38,7 @@ KERNELS = {"byte": KERNEL_BYTE, "bit": KERNEL_BIT}
 XPORT_AUTO, XPORT_RCCL, XPORT_LOCAL = 0, 1, 2
 HALO_SEND, HALO_RECV, HALO_FILL = 0, 1, 2
 HALO_COLUMN, HALO_ROW = 0, 1
+OPT_SMALL_GRID, OPT_OVERLAP = 1, 2
 
 # Every symbol include/life_mi355x.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = (
@@ -46,7 +47,7 @@ ABI_SYMBOLS = (
     "life_get_unique_id", "life_dev_create_rank", "life_dev_upload", "life_dev_fill_random",
     "life_dev_step", "life_dev_gather", "life_dev_live_count", "life_dev_sync",
     "life_dev_layout", "life_dev_world", "life_dev_set_timing", "life_dev_kernel_stats",
-    "life_tune", "life_tune_temporal", "life_dev_destroy",
+    "life_tune", "life_tune_temporal", "life_dev_configure", "life_dev_destroy",
 )
 
 
@@ -110,6 +111,7 @@ def _lib():
         L.life_dev_layout.argtypes = [vp, i32, P(Layout)]
         L.life_dev_world.argtypes = [vp] + [P(ctypes.c_int)] * 5
         L.life_dev_set_timing.argtypes = [vp, i32]
+        L.life_dev_configure.argtypes = [vp, i32, i32]
         L.life_dev_kernel_stats.argtypes = [vp, P(ctypes.c_double), P(i64), P(ctypes.c_double)]
         L.life_tune.argtypes = [i32, i32, i32]
         L.life_tune_temporal.argtypes = [i32]
@@ -192,7 +194,7 @@ class Life:
     """
 
     def __init__(self, nx: int, ny: int, shards: int = 1, kernel="bit", dims=(0, 0),
-                 transport: int = XPORT_AUTO, _handle=None):
+                 transport: int = XPORT_AUTO, small_grid: bool = True, overlap: bool = True, _handle=None):
         self.nx, self.ny = int(nx), int(ny)
         self.kernel = kernel_id(kernel)
         self._h = ctypes.c_void_p()
@@ -201,6 +203,13 @@ class Life:
         else:
             _check(_lib().life_dev_create_ex(self.nx, self.ny, shards, dims[0], dims[1], self.kernel,
                                              transport, ctypes.byref(self._h)), "life_dev_create")
+        if not small_grid:
+            self.configure(OPT_SMALL_GRID, 0)
+        if not overlap:
+            self.configure(OPT_OVERLAP, 0)
+
+    def configure(self, option: int, value: int) -> None:
+        _check(_lib().life_dev_configure(self._h, option, value), "configure")
 
     @classmethod
     def for_rank(cls, nx, ny, rank, world, uid: bytes, device: int, kernel="bit", dims=(0, 0)):

@@ -40,9 +40,9 @@ __global__ __launch_bounds__(256) void ub_kernel(TArgs a) {
     constexpr int T = NR - 2 * kTK;
     const int lane = threadIdx.x & 63;
     const int64_t wv = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t ntx = a.tx1 - a.tx0;
-    const int64_t tx = a.tx0 + wv % ntx, ty = a.ty0 + wv / ntx;
-    if (ty >= a.ty1) return;
+    if (wv >= a.first[1]) return;
+    const int64_t ntx = a.tx1[0] - a.tx0[0];
+    const int64_t tx = a.tx0[0] + wv % ntx, ty = a.ty0[0] + wv / ntx;
     const int64_t j = tx * 62 + lane - 1;
     int64_t jl = j % a.W;
     if (jl < 0) jl += a.W;
@@ -93,12 +93,14 @@ float run(const life_layout &L, uint8_t *in, uint8_t *out, int reps) {
     a.W = L.w / 32;
     a.h = L.h;
     a.ya = L.yapron;
-    a.tx0 = 0;
-    a.tx1 = (a.W + 61) / 62;
-    a.ty0 = 0;
-    a.ty1 = (L.h + T - 1) / T;
+    a.nreg = 1;
+    a.tx0[0] = 0;
+    a.tx1[0] = (a.W + 61) / 62;
+    a.ty0[0] = 0;
+    a.first[0] = 0;
+    a.first[1] = a.tx1[0] * ((L.h + T - 1) / T);
     a.m = kTK;
-    const int64_t waves = a.tx1 * a.ty1;
+    const int64_t waves = a.first[1];
     const unsigned grid = (unsigned)((waves + 3) / 4);
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);

@@ -42,11 +42,12 @@ def test_pattern_every_frame(gpu, name, kernel, shards):
             life.step(1)
 
 
+@pytest.mark.parametrize("small", [False, True], ids=["stream", "lds"])
 @pytest.mark.parametrize("kernel", ["byte", "bit"])
-def test_p46gun_big_gen10000(gpu, kernel):
+def test_p46gun_big_gen10000(gpu, kernel, small):
     """configs[1] at full length: md5 28998c4b... (549 live) after 10000 generations."""
     _, _, grid = gpu.load_cfg(os.path.join(GOLDEN, "cfg", "p46gun_big.cfg"))
-    with gpu.Life(500, 500, kernel=kernel) as life:
+    with gpu.Life(500, 500, kernel=kernel, small_grid=small) as life:
         life.upload(grid)
         life.step(10000)
         g = life.gather()
@@ -58,7 +59,7 @@ def test_p46gun_big_gen10000(gpu, kernel):
 @pytest.mark.parametrize("case", G["random"], ids=lambda c: f'{c["nx"]}x{c["ny"]}s{c["seed"]}')
 def test_random_vs_reference_life_step(gpu, kernel, case):
     nx, ny = case["nx"], case["ny"]
-    with gpu.Life(nx, ny, kernel=kernel) as life:
+    with gpu.Life(nx, ny, kernel=kernel, small_grid=False) as life:
         life.fill_random(case["seed"], case["density"])
         assert md5(life.gather().tobytes()) == case["init_md5"]
         done = 0

@@ -12,11 +12,14 @@ SIZES = [(1, 1), (1, 5), (5, 1), (2, 3), (3, 2), (16, 16), (17, 3), (31, 33), (6
          (65, 65), (127, 5), (128, 128), (129, 130), (200, 1), (1000, 37), (257, 300)]
 
 
+@pytest.mark.parametrize("small", [False, True], ids=["stream", "lds"])
 @pytest.mark.parametrize("kernel", ["byte", "bit"])
 @pytest.mark.parametrize("nx,ny", SIZES)
-def test_single_shard(gpu, oracle, kernel, nx, ny):
+def test_single_shard(gpu, oracle, kernel, nx, ny, small):
+    """stream: the HBM-streaming kernels (one-generation or temporal);
+    lds: the LDS-resident small-grid path."""
     g0 = oracle.fill_random(nx, ny, seed=nx * 1000 + ny, density=0.4)
-    with gpu.Life(nx, ny, shards=1, kernel=kernel) as life:
+    with gpu.Life(nx, ny, shards=1, kernel=kernel, small_grid=small) as life:
         life.upload(g0)
         np.testing.assert_array_equal(life.gather(), g0)
         life.step(1)
@@ -62,7 +65,7 @@ def test_byte_equals_bit_long(gpu, oracle):
     g0 = oracle.fill_random(nx, ny, seed=11, density=0.5)
     out = {}
     for k in ("byte", "bit"):
-        with gpu.Life(nx, ny, kernel=k) as life:
+        with gpu.Life(nx, ny, kernel=k, small_grid=False) as life:
             life.upload(g0)
             life.step(gens)
             out[k] = life.gather()
@@ -76,7 +79,7 @@ def test_timing_stats(gpu, kernel, nx, launches, gens):
     """One timed launch per generation (one-generation kernels) or per up to
     8 generations (temporal bit kernel); bytes = 0.25 B (bit) / 2 B (byte)
     per cell-update the timed launches performed."""
-    with gpu.Life(nx, 4096, kernel=kernel) as life:
+    with gpu.Life(nx, 4096, kernel=kernel, small_grid=False) as life:
         life.fill_random(1)
         life.set_timing(True)
         life.step(gens)
@@ -93,7 +96,7 @@ def test_temporal_single_shard(gpu, oracle, nx, ny):
     generations per launch); runs of 1, 7, 8, 9 and 20 generations."""
     assert gpu.layout_query(nx, ny, (1, 1), 0, "bit").generations_per_exchange == 8
     g0 = oracle.fill_random(nx, ny, seed=nx + 3 * ny, density=0.5)
-    with gpu.Life(nx, ny, kernel="bit") as life:
+    with gpu.Life(nx, ny, kernel="bit", small_grid=False) as life:
         life.upload(g0)
         done = 0
         for n in (1, 7, 8, 9, 20):
@@ -129,9 +132,37 @@ def test_temporal_tile_heights_agree(gpu, oracle, rows):
     g0 = oracle.fill_random(nx, ny, seed=rows, density=0.5)
     gpu.tune_temporal(rows)
     try:
-        with gpu.Life(nx, ny, kernel="bit") as life:
+        with gpu.Life(nx, ny, kernel="bit", small_grid=False) as life:
             life.upload(g0)
             life.step(29)
             np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, 29, threads=4))
     finally:
         gpu.tune_temporal(96)
+
+
+# ---------------------------------------------------------------- LDS-resident small grids
+@pytest.mark.parametrize("kernel", ["bit", "byte"])
+@pytest.mark.parametrize("nx,ny,gens", [(500, 500, 300), (1, 1, 5), (33, 2, 17), (31, 31, 40), (1000, 600, 50),
+                                        (32768, 19, 9), (64, 3, 100), (97, 1, 12)])
+def test_small_grid_path(gpu, oracle, kernel, nx, ny, gens):
+    g0 = oracle.fill_random(nx, ny, seed=nx ^ ny, density=0.4)
+    with gpu.Life(nx, ny, kernel=kernel) as life:
+        life.upload(g0)
+        life.step(gens)
+        np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, gens, threads=4))
+        life.step(1)
+        np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, gens + 1, threads=4))
+
+
+@pytest.mark.parametrize("kernel", ["bit", "byte"])
+def test_repeated_gather_is_stable(gpu, oracle, kernel):
+    """Host transfers: 12 gathers of a 16 MiB grid into fresh pageable buffers
+    all equal the oracle (guards the blocking-copy rule of life_dev_gather)."""
+    want = oracle.fill_random(4096, 4096, 1, 0.5)
+    with gpu.Life(4096, 4096, kernel=kernel, small_grid=False) as life:
+        life.upload(want)
+        for _ in range(6):
+            np.testing.assert_array_equal(life.gather(), want)
+        life.fill_random(1, 0.5)
+        for _ in range(6):
+            np.testing.assert_array_equal(life.gather(), want)
