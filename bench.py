@@ -41,13 +41,17 @@ lm._lib()
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# VALU issue peak: 256 CUs x 4 SIMDs x 32 lanes/cycle (a wave64 instruction
+# issues over 2 cycles, MI355X_MICROARCH.md "Wave scheduling") x 2.4 GHz.
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=100)
-    p.add_argument("--warmup", type=int, default=10)
+    # defaults: whole multiples of the temporal kernel's 16 generations per launch
+    p.add_argument("--steps", type=int, default=160)
+    p.add_argument("--warmup", type=int, default=16)
     p.add_argument("--kernel", default="bit", choices=["bit", "byte"])
     p.add_argument("--size", type=int, default=65536, help="per-GPU block edge (weak scaling)")
     p.add_argument("--workload", default="weak", choices=["weak", "p46gun_big"])
@@ -90,13 +94,14 @@ def cpu_baseline(target_s: float):
     return res
 
 
-def load_traffic(kernel: str, size: int):
-    """HBM bytes per stencil launch from the committed rocprofv3 PMC summary."""
+def load_traffic(variant: str, size: int):
+    """HBM bytes per stencil launch from the committed rocprofv3 PMC summary
+    (scripts/traffic_summary.py); None where the access width is uncalibrated."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as f:
             t = json.load(f)
-        return t.get(f"{kernel}_{size}")
+        return t.get(f"{variant}_{size}")
     except (OSError, ValueError):
         return None
 
@@ -158,13 +163,18 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     avg_ms, launches, bytes_per_launch = life.kernel_stats()
+    updates_per_launch, valu_per_launch = life.kernel_work()
     live = life.live_count()
 
     if rank == 0:
         cells = float(nx) * float(ny) * a.steps
         value = cells / elapsed / 1e9
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-        traffic = load_traffic(a.kernel, a.size) if a.workload == "weak" else None
+        gens_per_launch = updates_per_launch / (bytes_per_launch / (0.25 if a.kernel == "bit" else 2.0)) \
+            if bytes_per_launch > 0 else 0.0
+        temporal = life.layout().generations_per_exchange > 1
+        variant = a.kernel + ("_temporal" if temporal else ("_onegen" if a.kernel == "bit" else ""))
+        traffic = load_traffic(variant, a.size) if a.workload == "weak" else None
         out = {
             "metric": "Gcell-updates/sec at 1/2/4/8 MI355X + % of HBM roofline, bit-exact",
             "value": round(value, 3),
@@ -184,8 +194,23 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel_avg_ms": round(avg_ms, 5), "kernel_launches": launches,
-                         "bytes_per_launch": bytes_per_launch},
+                         "bytes_per_launch": bytes_per_launch,
+                         "generations_per_launch": round(gens_per_launch, 3),
+                         # SURVEY 8(d)'s per-update figure (0.25 B bit / 2 B byte) x the
+                         # cell-updates of a launch: above the HBM peak once a launch
+                         # advances K > 1 generations per pass over HBM
+                         "per_generation_equivalent_GBps": round(
+                             updates_per_launch * (0.25 if a.kernel == "bit" else 2.0) / (avg_ms * 1e-3) / 1e9, 1)
+                         if avg_ms > 0 else 0.0},
         }
+        if valu_per_launch > 0 and avg_ms > 0:
+            # the temporally blocked kernel is VALU-issue bound, not HBM bound
+            tops = valu_per_launch / (avg_ms * 1e-3) / 1e12
+            out["valu"] = {"bound": "valu", "achieved": round(tops, 2), "peak": round(VALU_PEAK_TOPS, 2),
+                           "unit": "Tlane-op/s", "frac": round(tops / VALU_PEAK_TOPS, 4),
+                           "ops_per_launch": valu_per_launch, "model": "14 VALU ops per register row "
+                           "and generation (life_kernels.hip tstep_valu_per_tile_lane), within 3% of "
+                           "SQ_INSTS_VALU (profiles/r01/pmc_SQ_bit_temporal.csv)"}
         if n_gpus == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
         print(json.dumps(out), flush=True)

@@ -89,9 +89,10 @@ int life_halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int k
  * y + yapron at cell offset x from byte `xoff` (bit encoding: bit x&31 of the
  * little-endian dword (x>>5), floor division, counted from xoff).
  * `generations_per_exchange` is how many generations one halo exchange
- * feeds: 1 for the one-cell apron, LIFE_TEMPORAL_DEPTH for the bit-packed
- * temporally blocked stencil (32-cell x-apron, 8-row y-apron). */
-#define LIFE_TEMPORAL_DEPTH 8
+ * feeds: 1 for the one-cell apron, K = LIFE_TEMPORAL_DEPTH (16; 8 or 16 from
+ * the environment variable of the same name) for the bit-packed temporally
+ * blocked stencil (32-cell x-apron, K-row y-apron). */
+#define LIFE_TEMPORAL_DEPTH 16
 typedef struct {
     int64_t w, h;      /* owned block */
     int64_t x0, y0;    /* global origin of the block */
@@ -179,6 +180,13 @@ int life_dev_set_timing(life_dev *d, int on);
 #define LIFE_OPT_OVERLAP 2
 int life_dev_configure(life_dev *d, int option, int value);
 int life_dev_kernel_stats(life_dev *d, double *avg_ms, int64_t *launches, double *bytes_per_launch);
+/* The same timed launches: mean cell-updates per launch (cells x generations
+ * it advanced) and mean VALU lane-operations per launch (op-count model of
+ * the temporal bit stencil; 0 for the HBM-bound one-generation kernels).
+ * bytes_per_launch above is the COMPULSORY HBM traffic: one read + one write
+ * of every updated cell's encoding per launch, so a temporally blocked launch
+ * advancing K generations books its cells once, not K times. */
+int life_dev_kernel_work(life_dev *d, double *cell_updates_per_launch, double *valu_ops_per_launch);
 
 /* Stencil tuning for the whole process, per kernel family (-1: both): rows
  * each lane walks (16/32/64) and rows of loads kept in flight (2/4/8); 0
@@ -186,9 +194,10 @@ int life_dev_kernel_stats(life_dev *d, double *avg_ms, int64_t *launches, double
  * LIFE_STEP_ROWS / LIFE_STEP_DEPTH override them at load time. */
 int life_tune(int kernel, int rows, int depth);
 
-/* Temporal (bit, generations_per_exchange > 1) tile height: registers rows
- * per lane, 48/64/80/96 (tile = rows - 2*LIFE_TEMPORAL_DEPTH owned rows);
- * 0 keeps the current value; LIFE_TEMPORAL_ROWS overrides at load time. */
+/* Temporal (bit, generations_per_exchange = K > 1) tile height: register
+ * rows per wave, 32/48/64/80/96; a tile is one workgroup of 8 vertically
+ * stacked waves, 8*rows - 2K owned rows; 0 keeps the current value;
+ * LIFE_TEMPORAL_ROWS overrides at load time. */
 int life_tune_temporal(int rows);
 
 /* life_free (life_cart.c:146-157). */

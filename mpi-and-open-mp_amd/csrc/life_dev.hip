@@ -100,7 +100,9 @@ struct life_dev {
     std::vector<Shard> shards;
     double acc_ms = 0.0;
     int64_t acc_launches = 0;
-    double acc_bytes = 0.0;
+    double acc_bytes = 0.0;    // algorithmic HBM bytes of the timed launches
+    double acc_updates = 0.0;  // cell-updates they performed
+    double acc_valu = 0.0;     // VALU lane-ops they issue (model; 0 where not modelled)
 };
 
 namespace {
@@ -109,7 +111,8 @@ life::Wrap wrap_of(const life_dev *d) { return life::Wrap{d->dims[0] == 1, d->di
 
 int shard_alloc(life_dev *d, Shard &s) {
     HIPCHK(hipSetDevice(s.device));
-    const size_t bytes = (size_t)(s.lay.pitch * s.lay.rows);
+    const int64_t slack = s.lay.generations_per_exchange > 1 ? life::kTemporalSlackRows : 0;
+    const size_t bytes = (size_t)(s.lay.pitch * (s.lay.rows + slack));
     for (int i = 0; i < 2; i++) {
         HIPCHK(hipMalloc(&s.buf[i], bytes));
         HIPCHK(hipMemset(s.buf[i], 0, bytes));
@@ -319,7 +322,9 @@ int launch_region(life_dev *d, Shard &s, const life::Region &r, bool timed, hipS
         const bool bit = s.lay.kernel == LIFE_KERNEL_BIT;
         const int64_t cpu = bit ? 128 : 16;
         const int64_t xa = r.u0 * cpu, xb = r.u1 * cpu < s.lay.w ? r.u1 * cpu : s.lay.w;
-        d->acc_bytes += (double)(xb - xa) * (double)(r.r1 - r.r0) * (bit ? 0.25 : 2.0);
+        const double cells = (double)(xb - xa) * (double)(r.r1 - r.r0);
+        d->acc_bytes += cells * (bit ? 0.25 : 2.0);
+        d->acc_updates += cells;
     }
     return LIFE_OK;
 }
@@ -361,8 +366,16 @@ int launch_tiles(life_dev *d, Shard &s, const life::TileRegion *r, int nreg, int
         for (int k = 0; k < nreg; k++) {
             const int64_t wa = r[k].tx0 * g.words, wb = r[k].tx1 * g.words < W ? r[k].tx1 * g.words : W;
             const int64_t ya = r[k].ty0 * g.rows, yb = r[k].ty1 * g.rows < s.lay.h ? r[k].ty1 * g.rows : s.lay.h;
-            if (wb > wa && yb > ya)  // algorithmic bytes of the cell-updates performed (0.25 B each)
-                d->acc_bytes += (double)(wb - wa) * 32.0 * (double)(yb - ya) * (double)m * 0.25;
+            if (wb > wa && yb > ya) {
+                // compulsory HBM bytes of the launch: each owned cell's bit is
+                // read once and written once per m-generation pass (0.25 B),
+                // not once per generation -- that is the point of the blocking
+                const double cells = (double)(wb - wa) * 32.0 * (double)(yb - ya);
+                d->acc_bytes += cells * 0.25;
+                d->acc_updates += cells * (double)m;
+            }
+            const double tiles = (double)(r[k].tx1 - r[k].tx0) * (double)(r[k].ty1 - r[k].ty0);
+            d->acc_valu += tiles * 64.0 * life::tstep_valu_per_tile_lane(m);
         }
     }
     return LIFE_OK;
@@ -663,8 +676,10 @@ static int step_small(life_dev *d, int64_t generations) {
     HIPCHK(life::launch_small(s.lay, s.buf[s.cur], s.buf[s.cur ^ 1], generations, s.stream));
     if (t) {
         HIPCHK(hipEventRecord(t->b, s.stream));
-        d->acc_bytes += (double)s.lay.w * (double)s.lay.h * (double)generations *
-                        (s.lay.kernel == LIFE_KERNEL_BIT ? 0.25 : 2.0);
+        // LDS-resident: HBM sees one import and one export of the grid per launch
+        const double cells = (double)s.lay.w * (double)s.lay.h;
+        d->acc_bytes += cells * (s.lay.kernel == LIFE_KERNEL_BIT ? 0.25 : 2.0);
+        d->acc_updates += cells * (double)generations;
     }
     s.cur ^= 1;
     return LIFE_OK;
@@ -807,6 +822,17 @@ int life_dev_set_timing(life_dev *d, int on) {
     d->acc_ms = 0.0;
     d->acc_launches = 0;
     d->acc_bytes = 0.0;
+    d->acc_updates = 0.0;
+    d->acc_valu = 0.0;
+    return LIFE_OK;
+}
+
+int life_dev_kernel_work(life_dev *d, double *cell_updates_per_launch, double *valu_ops_per_launch) {
+    if (!d) return LIFE_EINVAL;
+    CHK(harvest_timers(d));
+    const double n = d->acc_launches ? (double)d->acc_launches : 1.0;
+    if (cell_updates_per_launch) *cell_updates_per_launch = d->acc_updates / n;
+    if (valu_ops_per_launch) *valu_ops_per_launch = d->acc_valu / n;
     return LIFE_OK;
 }
 
@@ -829,7 +855,7 @@ int life_tune(int kernel, int rows, int depth) {
 }
 
 int life_tune_temporal(int rows) {
-    if (rows && rows != 48 && rows != 64 && rows != 80 && rows != 96) return LIFE_EINVAL;
+    if (rows && rows != 32 && rows != 48 && rows != 64 && rows != 80 && rows != 96) return LIFE_EINVAL;
     life::set_temporal_rows(rows);
     return LIFE_OK;
 }

@@ -46,9 +46,9 @@ struct StepTuning {
 StepTuning step_tuning(bool bit);
 void set_step_tuning(int kernel, int rows, int depth);  // kernel -1: both
 
-// Temporally blocked bit stencil (layouts with generations_per_exchange ==
-// LIFE_TEMPORAL_DEPTH): tiles of 62 words x `rows` rows, m <= K generations
-// per launch from `in` to `out`.
+// Temporally blocked bit stencil (layouts with generations_per_exchange = K
+// in {8, 16}): tiles of 62 words x `rows` rows (one workgroup each), m <= K
+// generations per launch from `in` to `out`.
 struct TileRegion {
     int64_t tx0, tx1, ty0, ty1;
 };
@@ -56,10 +56,18 @@ struct TileGeom {
     int64_t words, rows, ntx, nty;
 };
 TileGeom tile_geom(const life_layout &L);
+// Rows a temporally blocked buffer is allocated beyond its layout's `rows`:
+// the last tile's window (<= 8 waves x 96 rows) may read past the bottom
+// apron without clamping.
+constexpr int64_t kTemporalSlackRows = 8 * 96;
 // Up to 4 disjoint tile regions in one launch.
 hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, const TileRegion *r, int nreg,
                         int m, Wrap wrap, hipStream_t s);
-int temporal_rows();              // registers rows per lane (48/64/80/96)
+int temporal_rows();              // register rows per wave (32/48/64/80/96)
+// VALU instructions the lanes at one lane position of a tile's waves issue
+// for m generations (the op-count model of life_kernels.hip tstep_kernel,
+// checked against the SQ_INSTS_VALU counter in profiles/); x 64 lanes x tiles.
+double tstep_valu_per_tile_lane(int m);
 void set_temporal_rows(int nr);
 
 // LDS-resident path for small single-shard grids: all `gens` generations in

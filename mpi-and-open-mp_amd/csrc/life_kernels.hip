@@ -297,24 +297,34 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs a) {
 }
 
 // ------------------------------------------------------------------ temporal
-// Temporally blocked bit stencil (layouts with generations_per_exchange > 1).
-// One wave owns a tile of 62 word columns x T rows: lane l holds word column
-// 62*tx + l - 1 (lanes 0 and 63 are the one-word x-apron of the tile) for
-// NR = T + 2K consecutive rows in NR registers, runs m <= K generations
-// there, and stores rows [K, K+T) of lanes 1..62.  After m generations the
-// wrong values that enter at the tile's edge rows / edge lanes have moved m
-// rows / m bits inward: rows [K, K+T) and lanes 1..62 (32 bits of margin) are
-// still exact.  HBM traffic per m generations: NR rows read + T rows written
-// per 62 columns, instead of 2 x m full passes.
-constexpr int kTK = LIFE_TEMPORAL_DEPTH;
-
+// Temporally blocked bit stencil (layouts with generations_per_exchange = K
+// > 1): m <= K generations per launch, each cell's bit read once from and
+// written once to HBM per launch.
+//
+// One workgroup owns a tile of 62 word columns x T owned rows.  Its
+// kStackWaves waves are stacked vertically: wave i holds window rows
+// [i*R, (i+1)*R) of a (kStackWaves*R)-row window that starts K rows above the
+// tile (T = kStackWaves*R - 2K), one 32-cell word per lane and register row
+// (lane l holds word column 62*tx + l - 1; lanes 0 and 63 are the one-word
+// x-apron of the tile).  Each generation a wave publishes the horizontal sums
+// of its first and last row in LDS, one barrier, and takes its neighbours'
+// (the only values that cross waves); the window's own top/bottom K rows and
+// the edge lanes absorb the wrong values that enter from outside (K rows / K
+// <= 32 bits after K generations), so rows [K, K+T) of lanes 1..62 are exact.
+// Versus one wave per tile (K-row ghost zones per wave), the ghost rows are
+// paid once per workgroup: 2K of kStackWaves*R rows.
+//
+// VALU (MI355X): per register row and generation 2 DPP moves + 2 v_alignbit
+// (horizontal neighbours) + 10 v_bitop3 (full adder 2, rule 8);
+// scripts/ubench_row.hip prices the row at ~20.7 ns per SIMD at 16 waves/CU.
 constexpr int kMaxRegions = 4;
+constexpr int kStackWaves = 8;  // waves per workgroup (2 per SIMD)
 struct TArgs {
     const uint8_t *in;
     uint8_t *out;
     int64_t pitch, xoff, W, h, ya;  // W = 32-bit words per owned row
     // up to kMaxRegions tile regions in one launch (the boundary ring of a
-    // partitioned shard); wave w belongs to the region with first[k] <= w
+    // partitioned shard); workgroup b belongs to the region with first[k] <= b
     int64_t tx0[kMaxRegions], tx1[kMaxRegions], ty0[kMaxRegions], first[kMaxRegions + 1];
     int32_t nreg, m;
 };
@@ -334,38 +344,20 @@ __device__ __forceinline__ void bit_hsum(uint32_t v, uint32_t &s0, uint32_t &s1)
     BitEnc::fa(L, v, R, s0, s1);
 }
 
-// One generation over register rows [lo, hi) (rows outside keep their old,
-// no longer needed values; a row outside [0, NR) counts as dead).
-template <int NR>
-__device__ __forceinline__ void tgen_rows(uint32_t (&v)[NR], const int lo, const int hi) {
-    uint32_t p0 = 0u, p1 = 0u, c0, c1;
-    if (lo > 0) bit_hsum(v[lo - 1], p0, p1);
-    bit_hsum(v[lo], c0, c1);
-#pragma unroll
-    for (int r = lo; r < hi; ++r) {
-        uint32_t n0 = 0u, n1 = 0u;
-        if (r + 1 < NR) bit_hsum(v[r + 1], n0, n1);
-        v[r] = BitEnc::rule1(p0, p1, c0, c1, n0, n1, v[r]);
-        p0 = c0;
-        p1 = c1;
-        c0 = n0;
-        c1 = n1;
-    }
-}
-
-// (A fully unrolled variant that skips the rows generation g no longer
-// needs -- ghost-zone shrink, 11-14 % fewer ops -- spilled at every
-// occupancy bound tried on ROCm 7.2 and was dropped)
-template <int NR, bool WRAPX, bool WRAPY>
-__global__ __launch_bounds__(kBlock) void tstep_kernel(TArgs a) {
-    constexpr int T = NR - 2 * kTK;
+template <int R, int K, bool WRAPX, bool WRAPY>
+__global__ __launch_bounds__(64 * kStackWaves) void tstep_kernel(TArgs a) {
+    static_assert(R >= 3 && K >= 1 && K <= 32, "window");
+    constexpr int NW = kStackWaves;
+    constexpr int T = NW * R - 2 * K;
+    __shared__ uint32_t xch[2][NW][4][64];  // [parity][wave][top s0/s1, bottom s0/s1][lane]
     const int lane = threadIdx.x & 63;
     // wave index: uniform, so every row address below is scalar (SALU) math
-    const int64_t wv = (int64_t)blockIdx.x * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (wv >= a.first[a.nreg]) return;  // whole wave
+    const int wi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t wg = blockIdx.x;
+    if (wg >= a.first[a.nreg]) return;  // whole workgroup
     int k = 0;
-    while (k + 1 < a.nreg && wv >= a.first[k + 1]) ++k;
-    const int64_t ntx = a.tx1[k] - a.tx0[k], wr = wv - a.first[k];
+    while (k + 1 < a.nreg && wg >= a.first[k + 1]) ++k;
+    const int64_t ntx = a.tx1[k] - a.tx0[k], wr = wg - a.first[k];
     const int64_t tx = a.tx0[k] + wr % ntx, ty = a.ty0[k] + wr / ntx;
     const int64_t j = tx * 62 + lane - 1;  // word column of this lane
     int64_t jl;
@@ -376,33 +368,86 @@ __global__ __launch_bounds__(kBlock) void tstep_kernel(TArgs a) {
         jl = j > a.W ? a.W : j;  // words -1 .. W hold cells/apron; beyond: clamp (never stored)
     }
     const uint32_t voff = (uint32_t)(a.xoff + 4 * jl);
-    // first register row = owned row ty*T - K
-    int64_t y = ty * T - kTK;
+    const int64_t y0 = ty * T - K + (int64_t)wi * R;  // owned row of register row 0 (>= -K)
+    // Row pointers are walked: with a periodic y axis the walk wraps at h;
+    // with an apron the last tile's window may run past the apron row h+K-1
+    // into the allocation slack below the buffer (kTemporalSlackRows; those
+    // rows are never stored).
+    const uint8_t *row0 = a.in + a.ya * a.pitch;  // owned row 0
+    int64_t y = y0;
     if (WRAPY) {
         y %= a.h;
         if (y < 0) y += a.h;
     }
-    uint32_t v[NR];
+    const uint8_t *p = row0 + y * a.pitch;
+    uint32_t v[R];
 #pragma unroll
-    for (int r = 0; r < NR; ++r) {
-        int64_t yy = y;
-        if (!WRAPY) yy = y < -kTK ? -kTK : (y >= a.h + kTK ? a.h + kTK - 1 : y);
-        v[r] = *reinterpret_cast<const uint32_t *>(a.in + (yy + a.ya) * a.pitch + voff);
+    for (int r = 0; r < R; ++r) {
+        v[r] = *reinterpret_cast<const uint32_t *>(p + voff);
         ++y;
-        if (WRAPY && y == a.h) y = 0;
+        if (WRAPY) {
+            if (y == a.h) {
+                y = 0;
+                p = row0;
+            } else {
+                p += a.pitch;
+            }
+        } else {
+            p += a.pitch;
+        }
     }
-    for (int g = 0; g < a.m; ++g) tgen_rows<NR>(v, 0, NR);
+    for (int g = 0; g < a.m; ++g) {
+        const int par = g & 1;
+        uint32_t t0, t1, b0, b1;
+        bit_hsum(v[0], t0, t1);
+        bit_hsum(v[R - 1], b0, b1);
+        xch[par][wi][0][lane] = t0;
+        xch[par][wi][1][lane] = t1;
+        xch[par][wi][2][lane] = b0;
+        xch[par][wi][3][lane] = b1;
+        __syncthreads();
+        // the row above the window / below it: dead (window ghost rows)
+        uint32_t a0 = 0u, a1 = 0u, d0 = 0u, d1 = 0u;
+        if (wi > 0) {
+            a0 = xch[par][wi - 1][2][lane];
+            a1 = xch[par][wi - 1][3][lane];
+        }
+        if (wi < NW - 1) {
+            d0 = xch[par][wi + 1][0][lane];
+            d1 = xch[par][wi + 1][1][lane];
+        }
+        // rows 1 .. R-2 need only this wave's rows: they run while the LDS
+        // reads are in flight
+        uint32_t p0 = t0, p1 = t1, c0, c1;
+        bit_hsum(v[1], c0, c1);
+        const uint32_t h10 = c0, h11 = c1;
+#pragma unroll
+        for (int r = 1; r < R - 1; ++r) {
+            uint32_t n0, n1;
+            if (r + 1 == R - 1) {
+                n0 = b0;
+                n1 = b1;
+            } else {
+                bit_hsum(v[r + 1], n0, n1);
+            }
+            v[r] = BitEnc::rule1(p0, p1, c0, c1, n0, n1, v[r]);
+            p0 = c0;
+            p1 = c1;
+            c0 = n0;
+            c1 = n1;
+        }
+        v[R - 1] = BitEnc::rule1(p0, p1, b0, b1, d0, d1, v[R - 1]);
+        v[0] = BitEnc::rule1(a0, a1, t0, t1, h10, h11, v[0]);
+    }
     const bool st = lane >= 1 && lane <= 62 && j < a.W;
-    const int64_t yo = ty * T;  // owned row of register row K
-    uint8_t *dst = a.out + (yo + a.ya) * a.pitch + voff;
-    if (yo + T <= a.h) {
+    // window rows [K, NW*R - K) are the tile's owned rows [ty*T, ty*T + T)
+    const int r0 = wi == 0 ? K : 0, r1 = wi == NW - 1 ? R - K : R;
+    uint8_t *q = a.out + (a.ya + y0 + r0) * a.pitch + voff;
 #pragma unroll
-        for (int r = 0; r < T; ++r)
-            if (st) *reinterpret_cast<uint32_t *>(dst + r * a.pitch) = v[kTK + r];
-    } else {
-#pragma unroll
-        for (int r = 0; r < T; ++r)
-            if (st && yo + r < a.h) *reinterpret_cast<uint32_t *>(dst + r * a.pitch) = v[kTK + r];
+    for (int r = 0; r < R; ++r) {
+        if (r < r0 || r >= r1) continue;
+        if (st && y0 + r < a.h) *reinterpret_cast<uint32_t *>(q) = v[r];
+        q += a.pitch;
     }
 }
 
@@ -660,8 +705,8 @@ namespace {
 // byte R64/D2 were the fastest of {16,32,64} x {2,4,8}.
 struct Tunings {
     StepTuning t[2];  // [0] byte, [1] bit
-    int nr = 96;      // temporal tile: registers rows per lane (T = nr - 2K); fastest of
-                      // 48/64/80/96 at 65536^2 (profiles/r01/tune_temporal.jsonl)
+    int nr = 64;      // temporal stencil: register rows per wave (window = kStackWaves * nr
+                      // rows, tile = window - 2K); fastest measured at 65536^2
     Tunings() : t{{64, 2}, {16, 8}} {
         for (StepTuning &v : t) {
             if (const char *e = getenv("LIFE_STEP_ROWS")) v.rows = atoi(e);
@@ -674,17 +719,25 @@ Tunings &tunings() {
     static Tunings t;
     return t;
 }
+bool temporal_rows_ok(int nr) { return nr == 32 || nr == 48 || nr == 64 || nr == 80 || nr == 96; }
 }  // namespace
 
 StepTuning step_tuning(bool bit) { return tunings().t[bit ? 1 : 0]; }
 
 int temporal_rows() {
     const int nr = tunings().nr;
-    return nr == 48 || nr == 64 || nr == 80 ? nr : 96;
+    return temporal_rows_ok(nr) ? nr : 64;
+}
+
+// Per register row and generation: bit_hsum = 2 DPP moves + 2 v_alignbit +
+// 2 v_bitop3, rule1 = 8 v_bitop3; kStackWaves waves of temporal_rows() rows
+// per tile.
+double tstep_valu_per_tile_lane(int m) {
+    return 14.0 * (double)kStackWaves * (double)temporal_rows() * (double)m;
 }
 
 void set_temporal_rows(int nr) {
-    if (nr == 48 || nr == 64 || nr == 80 || nr == 96) tunings().nr = nr;
+    if (temporal_rows_ok(nr)) tunings().nr = nr;
 }
 
 void set_step_tuning(int kernel, int rows, int depth) {
@@ -751,25 +804,36 @@ hipError_t launch_step(const life_layout &L, const uint8_t *in, uint8_t *out, ui
 }
 
 namespace {
-template <int NR>
+template <int R, int K>
 hipError_t launch_t(const TArgs &a, Wrap wrap, unsigned grid, hipStream_t s) {
+    constexpr unsigned kThreads = 64 * kStackWaves;
     if (wrap.x && wrap.y)
-        tstep_kernel<NR, true, true><<<grid, kBlock, 0, s>>>(a);
+        tstep_kernel<R, K, true, true><<<grid, kThreads, 0, s>>>(a);
     else if (wrap.x)
-        tstep_kernel<NR, true, false><<<grid, kBlock, 0, s>>>(a);
+        tstep_kernel<R, K, true, false><<<grid, kThreads, 0, s>>>(a);
     else if (wrap.y)
-        tstep_kernel<NR, false, true><<<grid, kBlock, 0, s>>>(a);
+        tstep_kernel<R, K, false, true><<<grid, kThreads, 0, s>>>(a);
     else
-        tstep_kernel<NR, false, false><<<grid, kBlock, 0, s>>>(a);
+        tstep_kernel<R, K, false, false><<<grid, kThreads, 0, s>>>(a);
     return hipGetLastError();
+}
+
+template <int K>
+hipError_t launch_k(const TArgs &a, Wrap wrap, unsigned grid, hipStream_t s) {
+    switch (temporal_rows()) {
+    case 32: return launch_t<32, K>(a, wrap, grid, s);
+    case 48: return launch_t<48, K>(a, wrap, grid, s);
+    case 80: return launch_t<80, K>(a, wrap, grid, s);
+    case 96: return launch_t<96, K>(a, wrap, grid, s);
+    default: return launch_t<64, K>(a, wrap, grid, s);
+    }
 }
 }  // namespace
 
 TileGeom tile_geom(const life_layout &L) {
-    const int nr = temporal_rows();
     TileGeom g;
     g.words = 62;
-    g.rows = nr - 2 * kTK;
+    g.rows = (int64_t)kStackWaves * temporal_rows() - 2 * (int64_t)L.generations_per_exchange;
     g.ntx = (L.w / 32 + g.words - 1) / g.words;
     g.nty = (L.h + g.rows - 1) / g.rows;
     return g;
@@ -777,7 +841,8 @@ TileGeom tile_geom(const life_layout &L) {
 
 hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, const TileRegion *r, int nreg,
                         int m, Wrap wrap, hipStream_t s) {
-    if (nreg < 0 || nreg > kMaxRegions || m > kTK || L.generations_per_exchange != kTK) return hipErrorInvalidValue;
+    const int K = L.generations_per_exchange;
+    if (nreg < 0 || nreg > kMaxRegions || m > K || (K != 8 && K != 16) || L.yapron != K) return hipErrorInvalidValue;
     TArgs a;
     a.in = in;
     a.out = out;
@@ -798,14 +863,8 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
         a.first[n + 1] = a.first[n] + (r[k].tx1 - r[k].tx0) * (r[k].ty1 - r[k].ty0);
     }
     if (a.nreg == 0 || m <= 0) return hipSuccess;
-    const int64_t waves = a.first[a.nreg];
-    const unsigned grid = (unsigned)((waves + kBlock / 64 - 1) / (kBlock / 64));
-    switch (temporal_rows()) {
-    case 48: return launch_t<48>(a, wrap, grid, s);
-    case 64: return launch_t<64>(a, wrap, grid, s);
-    case 80: return launch_t<80>(a, wrap, grid, s);
-    default: return launch_t<96>(a, wrap, grid, s);
-    }
+    const unsigned grid = (unsigned)a.first[a.nreg];  // one workgroup per tile
+    return K == 16 ? launch_k<16>(a, wrap, grid, s) : launch_k<8>(a, wrap, grid, s);
 }
 
 int64_t small_lds_bytes(const life_layout &L) {

@@ -8,6 +8,7 @@
 // The corner messages are dropped: columns go first, then rows of width+2
 // carry the freshly received column apron (the corners) along.
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "life_mi355x.h"
@@ -36,8 +37,20 @@ void life_dims_create(int n, int dims[2]) {
     dims[1] = d1;
 }
 
+// Generations per halo exchange of the temporally blocked layout:
+// LIFE_TEMPORAL_DEPTH, or 8 / 16 from the environment variable of the same
+// name (read once; every rank of a job must see the same value).
+static int temporal_depth() {
+    static const int k = [] {
+        const char *e = getenv("LIFE_TEMPORAL_DEPTH");
+        const int v = e ? atoi(e) : 0;
+        return v == 8 || v == 16 ? v : LIFE_TEMPORAL_DEPTH;
+    }();
+    return k;
+}
+
 // The bit-packed temporally blocked stencil exchanges whole 32-cell words
-// in x and LIFE_TEMPORAL_DEPTH rows in y, and wraps a non-partitioned x axis
+// in x and K = temporal_depth() rows in y, and wraps a non-partitioned x axis
 // at word granularity: every block width must be a multiple of 32, and a
 // partitioned y axis needs blocks at least as tall as the apron it feeds.
 static bool temporal_ok(int64_t nx, int64_t ny, int dims0, int dims1) {
@@ -50,7 +63,7 @@ static bool temporal_ok(int64_t nx, int64_t ny, int dims0, int dims1) {
         for (int k = 0; k < dims1; k++) {
             int64_t s, e;
             life_decomposition(ny, dims1, k, &s, &e);
-            if (e - s < LIFE_TEMPORAL_DEPTH) return false;
+            if (e - s < temporal_depth()) return false;
         }
     return true;
 }
@@ -75,8 +88,8 @@ int life_layout_query(int64_t nx, int64_t ny, int dims0, int dims1, int rank, in
     out->coords[1] = c1;
     const bool temporal = kernel == LIFE_KERNEL_BIT && temporal_ok(nx, ny, dims0, dims1);
     out->xapron = temporal ? 32 : 1;
-    out->yapron = temporal ? LIFE_TEMPORAL_DEPTH : 1;
-    out->generations_per_exchange = temporal ? LIFE_TEMPORAL_DEPTH : 1;
+    out->yapron = temporal ? temporal_depth() : 1;
+    out->generations_per_exchange = temporal ? temporal_depth() : 1;
     const int64_t cells_per_unit = kernel == LIFE_KERNEL_BIT ? 128 : 16;
     out->units = (out->w + cells_per_unit - 1) / cells_per_unit;
     out->xoff = kXoff;

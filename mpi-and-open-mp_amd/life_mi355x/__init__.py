@@ -39,6 +39,7 @@ XPORT_AUTO, XPORT_RCCL, XPORT_LOCAL = 0, 1, 2
 HALO_SEND, HALO_RECV, HALO_FILL = 0, 1, 2
 HALO_COLUMN, HALO_ROW = 0, 1
 OPT_SMALL_GRID, OPT_OVERLAP = 1, 2
+TEMPORAL_DEPTH = 16  # LIFE_TEMPORAL_DEPTH: generations per halo exchange of the temporal layout
 
 # Every symbol include/life_mi355x.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = (
@@ -47,7 +48,7 @@ ABI_SYMBOLS = (
     "life_get_unique_id", "life_dev_create_rank", "life_dev_upload", "life_dev_fill_random",
     "life_dev_step", "life_dev_gather", "life_dev_live_count", "life_dev_sync",
     "life_dev_layout", "life_dev_world", "life_dev_set_timing", "life_dev_kernel_stats",
-    "life_tune", "life_tune_temporal", "life_dev_configure", "life_dev_destroy",
+    "life_tune", "life_tune_temporal", "life_dev_configure", "life_dev_kernel_work", "life_dev_destroy",
 )
 
 
@@ -113,6 +114,7 @@ def _lib():
         L.life_dev_set_timing.argtypes = [vp, i32]
         L.life_dev_configure.argtypes = [vp, i32, i32]
         L.life_dev_kernel_stats.argtypes = [vp, P(ctypes.c_double), P(i64), P(ctypes.c_double)]
+        L.life_dev_kernel_work.argtypes = [vp, P(ctypes.c_double), P(ctypes.c_double)]
         L.life_tune.argtypes = [i32, i32, i32]
         L.life_tune_temporal.argtypes = [i32]
         L.life_dev_destroy.argtypes = [vp]
@@ -261,6 +263,12 @@ class Life:
         _check(_lib().life_dev_kernel_stats(self._h, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(b)),
                "kernel_stats")
         return ms.value, n.value, b.value
+
+    def kernel_work(self):
+        """(cell-updates, VALU lane-ops) per timed launch (life_dev_kernel_work)."""
+        u, v = ctypes.c_double(), ctypes.c_double()
+        _check(_lib().life_dev_kernel_work(self._h, ctypes.byref(u), ctypes.byref(v)), "kernel_work")
+        return u.value, v.value
 
     def close(self) -> None:
         if self._h:

@@ -1,11 +1,20 @@
 #!/usr/bin/env python3
-"""profiles/<round>/pmc_*_<kernel>.csv -> profiles/traffic.json.
+"""profiles/<round>/pmc_{FETCH,WRITE}_SIZE_<variant>.csv -> profiles/traffic.json.
 
 HBM bytes per stencil launch from rocprofv3 FETCH_SIZE / WRITE_SIZE (KiB per
-dispatch), corrected as MI355X_MICROARCH.md's HBM section prescribes for
-gfx950: FETCH_SIZE reports half the bytes of wide (16 B/lane) coalesced
-streaming reads, so it is doubled; WRITE_SIZE is exact for 16-B streaming
-stores.  Each counter came from its own --pmc pass.
+dispatch, each counter from its own --pmc pass), read as
+MI355X_MICROARCH.md's HBM section prescribes for gfx950:
+
+* 16-B-per-lane streaming kernels (step_kernel, byte and one-generation
+  bit): FETCH_SIZE reports half the bytes of wide coalesced reads, so it is
+  doubled; WRITE_SIZE is exact for 16-B streaming stores.
+* the temporal bit kernel (tstep_kernel) loads and stores 4 B per lane:
+  an access width the guide lists as uncalibrated, so its entry carries the
+  raw counter values and `calibrated: false`, and bench.py reports its
+  `traffic` as null rather than an unverified absolute.
+
+Only full-length launches are summarised (the median over the dispatches of
+the dominant kernel).
 """
 import csv
 import json
@@ -17,21 +26,43 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 rnd = sys.argv[1] if len(sys.argv) > 1 else "r01"
 size = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
 d = os.path.join(ROOT, "profiles", rnd)
+
+VARIANTS = {  # variant -> (kernel-name substring, calibrated 16-B access)
+    "bit_onegen": ("step_kernel<life::(anonymous namespace)::BitEnc", True),
+    "byte": ("step_kernel<life::(anonymous namespace)::ByteEnc", True),
+    "bit_temporal": ("tstep_kernel", False),
+}
+
 out = {}
-for k in ("bit", "byte"):
+for var, (needle, calibrated) in VARIANTS.items():
     vals = {}
     for c in ("FETCH_SIZE", "WRITE_SIZE"):
-        p = os.path.join(d, f"pmc_{c}_{k}.csv")
+        p = os.path.join(d, f"pmc_{c}_{var}.csv")
         if not os.path.exists(p):
             continue
-        v = [float(r["Counter_Value"]) for r in csv.DictReader(open(p)) if "step_kernel" in r["Kernel_Name"]]
-        vals[c] = statistics.median(v) * 1024.0
-    if len(vals) == 2:
+        rows = [r for r in csv.DictReader(open(p)) if needle in r["Kernel_Name"] and r["Counter_Name"] == c]
+        if not rows:
+            continue
+        # the longest dispatches are the full-length launches
+        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
+        full = [float(r["Counter_Value"]) for r, t in zip(rows, durs) if t >= 0.8 * max(durs)]
+        vals[c] = statistics.median(full) * 1024.0
+    if len(vals) != 2:
+        continue
+    key = f"{var}_{size}"
+    if calibrated:
         fetch = 2.0 * vals["FETCH_SIZE"]
-        out[f"{k}_{size}"] = round(fetch + vals["WRITE_SIZE"])
-        out[f"{k}_{size}_detail"] = {"fetch_bytes_corrected": round(fetch), "fetch_size_raw_bytes": round(vals["FETCH_SIZE"]),
-                                     "write_bytes": round(vals["WRITE_SIZE"]), "source": f"profiles/{rnd}/pmc_*_{k}.csv",
-                                     "correction": "FETCH_SIZE x2 (gfx950, 16 B/lane streaming reads)"}
+        out[key] = round(fetch + vals["WRITE_SIZE"])
+        out[key + "_detail"] = {"fetch_bytes_corrected": round(fetch), "fetch_size_raw_bytes": round(vals["FETCH_SIZE"]),
+                                "write_bytes": round(vals["WRITE_SIZE"]), "source": f"profiles/{rnd}/pmc_*_{var}.csv",
+                                "correction": "FETCH_SIZE x2 (gfx950, 16 B/lane streaming reads)", "calibrated": True}
+    else:
+        out[key] = None
+        out[key + "_detail"] = {"fetch_size_raw_bytes": round(vals["FETCH_SIZE"]),
+                                "write_size_raw_bytes": round(vals["WRITE_SIZE"]),
+                                "source": f"profiles/{rnd}/pmc_*_{var}.csv", "calibrated": False,
+                                "note": "4 B/lane loads and stores: access width uncalibrated on gfx950 "
+                                        "(MI355X_MICROARCH.md, HBM); raw counter values, not HBM bytes"}
 with open(os.path.join(ROOT, "profiles", "traffic.json"), "w") as f:
     json.dump(out, f, indent=1)
 print(json.dumps(out, indent=1))

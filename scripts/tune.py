@@ -29,25 +29,27 @@ a = p.parse_args()
 if a.temporal:
     heights = [int(v) for v in a.temporal.split(",")]
     life = lm.Life(a.size, a.size, kernel="bit")
+    K = life.layout().generations_per_exchange
     life.fill_random(1, 0.5)
     res = {v: [] for v in heights}
     for rnd in range(a.rounds):
         for v in heights:
             lm.tune_temporal(v)
-            life.step(8)
+            life.step(K)
             life.sync()
             life.set_timing(True)
-            life.step(8 * a.gens)
+            life.step(K * a.gens)
             ms, n, b = life.kernel_stats()
+            upd, valu = life.kernel_work()
             life.set_timing(False)
-            res[v].append((ms, b))
+            res[v].append((ms, b, upd, valu))
     for v in heights:
-        mss = [m for m, _ in res[v]]
-        b = res[v][0][1]
-        med = statistics.median(mss)
-        print(json.dumps({"kernel": "bit-temporal", "rows": v, "median_ms_per_launch": round(med, 4),
-                          "gens_per_launch": 8, "Gcells_per_s": round(b / 0.25 / med / 1e6, 1),
-                          "alg_GBps": round(b / med / 1e6, 1)}), flush=True)
+        med = statistics.median(m for m, *_ in res[v])
+        _, b, upd, valu = res[v][0]
+        print(json.dumps({"kernel": "bit-temporal", "rows_per_wave": v, "K": K, "median_ms_per_launch": round(med, 4),
+                          "gens_per_launch": round(upd / (b / 0.25), 3), "Gcells_per_s": round(upd / med / 1e6, 1),
+                          "hbm_GBps": round(b / med / 1e6, 1), "valu_Tops": round(valu / med / 1e9, 2),
+                          "live": life.live_count()}), flush=True)
     life.close()
     sys.exit(0)
 

@@ -73,33 +73,41 @@ def test_byte_equals_bit_long(gpu, oracle):
     np.testing.assert_array_equal(out["bit"], oracle.life_run(g0, gens, threads=4))
 
 
-@pytest.mark.parametrize("kernel,nx,launches,gens", [("bit", 4096, 2, 13), ("bit", 4016, 13, 13),
+@pytest.mark.parametrize("kernel,nx,launches,gens", [("bit", 4096, 2, 20), ("bit", 4016, 13, 13),
                                                      ("byte", 4096, 13, 13)])
 def test_timing_stats(gpu, kernel, nx, launches, gens):
     """One timed launch per generation (one-generation kernels) or per up to
-    8 generations (temporal bit kernel); bytes = 0.25 B (bit) / 2 B (byte)
-    per cell-update the timed launches performed."""
+    8 generations (temporal bit kernel).  Bytes are the compulsory HBM
+    traffic: 0.25 B (bit) / 2 B (byte) per cell per LAUNCH; cell-updates are
+    cells x generations; VALU lane-ops are modelled for the temporal kernel
+    only (14 per register row per generation)."""
     with gpu.Life(nx, 4096, kernel=kernel, small_grid=False) as life:
         life.fill_random(1)
         life.set_timing(True)
         life.step(gens)
         ms, n, b = life.kernel_stats()
+        upd, valu = life.kernel_work()
         assert n == launches and ms > 0
-        assert n * b == pytest.approx(nx * 4096 * gens * (0.25 if kernel == "bit" else 2.0))
+        assert n * b == pytest.approx(nx * 4096 * launches * (0.25 if kernel == "bit" else 2.0))
+        assert n * upd == pytest.approx(nx * 4096 * gens)
+        temporal = launches < gens
+        assert (valu > 0) == temporal
+        if temporal:  # 3 x 9 tiles of 62 words x 480 rows (8 waves x 64 rows - 2K), 64 lanes
+            assert n * valu == pytest.approx(3 * 9 * 64 * 14 * 8 * 64 * gens)
 
 
 # ---------------------------------------------------------------- temporal blocking (bit)
 @pytest.mark.parametrize("nx,ny", [(32, 1), (32, 5), (64, 64), (96, 33), (2048, 100), (1024, 1000), (4096, 48),
                                    (32, 200), (1984, 130), (2016, 7)])
 def test_temporal_single_shard(gpu, oracle, nx, ny):
-    """Word-aligned widths take the temporally blocked kernel (up to 8
-    generations per launch); runs of 1, 7, 8, 9 and 20 generations."""
-    assert gpu.layout_query(nx, ny, (1, 1), 0, "bit").generations_per_exchange == 8
+    """Word-aligned widths take the temporally blocked kernel (up to K = 16
+    generations per launch); runs of 1, 7, 8, 9, 20 and 40 generations."""
+    assert gpu.layout_query(nx, ny, (1, 1), 0, "bit").generations_per_exchange == gpu.TEMPORAL_DEPTH
     g0 = oracle.fill_random(nx, ny, seed=nx + 3 * ny, density=0.5)
     with gpu.Life(nx, ny, kernel="bit", small_grid=False) as life:
         life.upload(g0)
         done = 0
-        for n in (1, 7, 8, 9, 20):
+        for n in (1, 7, 8, 9, 20, 40):
             life.step(n)
             done += n
             np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, done, threads=4),
@@ -107,26 +115,26 @@ def test_temporal_single_shard(gpu, oracle, nx, ny):
 
 
 @pytest.mark.parametrize("nx,ny,shards,dims", [
-    (256, 64, 4, (2, 2)), (512, 80, 8, (4, 2)), (64, 40, 4, (1, 4)), (256, 9, 4, (4, 1)), (64, 20, 2, (2, 1)),
-    (96, 16, 6, (3, 2)), (4096, 4096, 4, (2, 2)), (8192, 200, 8, (4, 2)),
+    (256, 64, 4, (2, 2)), (512, 80, 8, (4, 2)), (64, 80, 4, (1, 4)), (256, 9, 4, (4, 1)), (64, 20, 2, (2, 1)),
+    (96, 32, 6, (3, 2)), (4096, 4096, 4, (2, 2)), (8192, 200, 8, (4, 2)), (2048, 1100, 2, (1, 2)),
 ])
 def test_temporal_multi_shard_local(gpu, oracle, nx, ny, shards, dims):
-    """K-deep aprons through the LOCAL transport: whole-word columns, 8-row
+    """K-deep aprons through the LOCAL transport: whole-word columns, K-row
     blocks of rows, ring tiles first, interior overlapped with the exchange."""
     for r in range(shards):
-        assert gpu.layout_query(nx, ny, dims, r, "bit").generations_per_exchange == 8
+        assert gpu.layout_query(nx, ny, dims, r, "bit").generations_per_exchange == gpu.TEMPORAL_DEPTH
     g0 = oracle.fill_random(nx, ny, seed=7 * shards + ny, density=0.45)
     with gpu.Life(nx, ny, shards=shards, kernel="bit", dims=dims, transport=gpu.XPORT_LOCAL) as life:
         life.upload(g0)
         done = 0
-        for n in (1, 8, 13, 30):
+        for n in (1, 8, 13, 16, 30):
             life.step(n)
             done += n
             np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, done, threads=4),
                                           err_msg=f"after {done} generations")
 
 
-@pytest.mark.parametrize("rows", [48, 64, 80, 96])
+@pytest.mark.parametrize("rows", [32, 48, 64, 80, 96])
 def test_temporal_tile_heights_agree(gpu, oracle, rows):
     nx, ny = 2048, 333
     g0 = oracle.fill_random(nx, ny, seed=rows, density=0.5)
@@ -137,7 +145,7 @@ def test_temporal_tile_heights_agree(gpu, oracle, rows):
             life.step(29)
             np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, 29, threads=4))
     finally:
-        gpu.tune_temporal(96)
+        gpu.tune_temporal(64)
 
 
 # ---------------------------------------------------------------- LDS-resident small grids
