@@ -89,10 +89,12 @@ int life_halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int k
  * y + yapron at cell offset x from byte `xoff` (bit encoding: bit x&31 of the
  * little-endian dword (x>>5), floor division, counted from xoff).
  * `generations_per_exchange` is how many generations one halo exchange
- * feeds: 1 for the one-cell apron, K = LIFE_TEMPORAL_DEPTH (16; 8 or 16 from
- * the environment variable of the same name) for the bit-packed temporally
- * blocked stencil (32-cell x-apron, K-row y-apron). */
-#define LIFE_TEMPORAL_DEPTH 16
+ * feeds: 1 for the one-cell apron; for the temporally blocked stencil
+ * (32-cell x-apron, K-row y-apron) K = LIFE_TEMPORAL_DEPTH (bit) or
+ * LIFE_TEMPORAL_DEPTH_BYTE (byte), or 8/16/32 from the environment variables
+ * of the same names. */
+#define LIFE_TEMPORAL_DEPTH 32
+#define LIFE_TEMPORAL_DEPTH_BYTE 32
 typedef struct {
     int64_t w, h;      /* owned block */
     int64_t x0, y0;    /* global origin of the block */
@@ -194,11 +196,12 @@ int life_dev_kernel_work(life_dev *d, double *cell_updates_per_launch, double *v
  * LIFE_STEP_ROWS / LIFE_STEP_DEPTH override them at load time. */
 int life_tune(int kernel, int rows, int depth);
 
-/* Temporal (bit, generations_per_exchange = K > 1) tile height: register
- * rows per wave, 32/48/64/80/96; a tile is one workgroup of 8 vertically
- * stacked waves, 8*rows - 2K owned rows; 0 keeps the current value;
- * LIFE_TEMPORAL_ROWS overrides at load time. */
-int life_tune_temporal(int rows);
+/* Temporal (generations_per_exchange = K > 1) tile height of encoding
+ * `kernel` (-1: both): register rows per wave, 32/48/64/80/96; a tile is one
+ * workgroup of 8 vertically stacked waves, 8*rows - 2K owned rows; 0 keeps
+ * the current values (defaults bit 96, byte 48, by measurement);
+ * LIFE_TEMPORAL_ROWS / LIFE_TEMPORAL_ROWS_BYTE override at load time. */
+int life_tune_temporal(int kernel, int rows);
 
 /* life_free (life_cart.c:146-157). */
 void life_dev_destroy(life_dev *d);

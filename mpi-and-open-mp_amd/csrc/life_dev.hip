@@ -371,11 +371,11 @@ int launch_tiles(life_dev *d, Shard &s, const life::TileRegion *r, int nreg, int
                 // read once and written once per m-generation pass (0.25 B),
                 // not once per generation -- that is the point of the blocking
                 const double cells = (double)(wb - wa) * 32.0 * (double)(yb - ya);
-                d->acc_bytes += cells * 0.25;
+                d->acc_bytes += cells * (s.lay.kernel == LIFE_KERNEL_BIT ? 0.25 : 2.0);
                 d->acc_updates += cells * (double)m;
             }
             const double tiles = (double)(r[k].tx1 - r[k].tx0) * (double)(r[k].ty1 - r[k].ty0);
-            d->acc_valu += tiles * 64.0 * life::tstep_valu_per_tile_lane(m);
+            d->acc_valu += tiles * 64.0 * life::tstep_valu_per_tile_lane(m, s.lay.kernel == LIFE_KERNEL_BYTE);
         }
     }
     return LIFE_OK;
@@ -854,9 +854,11 @@ int life_tune(int kernel, int rows, int depth) {
     return LIFE_OK;
 }
 
-int life_tune_temporal(int rows) {
-    if (rows && rows != 32 && rows != 48 && rows != 64 && rows != 80 && rows != 96) return LIFE_EINVAL;
-    life::set_temporal_rows(rows);
+int life_tune_temporal(int kernel, int rows) {
+    if ((rows && rows != 32 && rows != 48 && rows != 64 && rows != 80 && rows != 96) || kernel < -1 ||
+        kernel > LIFE_KERNEL_BIT)
+        return LIFE_EINVAL;
+    life::set_temporal_rows(kernel, rows);
     return LIFE_OK;
 }
 

@@ -46,9 +46,9 @@ struct StepTuning {
 StepTuning step_tuning(bool bit);
 void set_step_tuning(int kernel, int rows, int depth);  // kernel -1: both
 
-// Temporally blocked bit stencil (layouts with generations_per_exchange = K
-// in {8, 16}): tiles of 62 words x `rows` rows (one workgroup each), m <= K
-// generations per launch from `in` to `out`.
+// Temporally blocked stencil (layouts with generations_per_exchange = K in
+// {8, 16}, either encoding): tiles of 62 32-cell word columns x `rows` rows
+// (one workgroup each), m <= K generations per launch from `in` to `out`.
 struct TileRegion {
     int64_t tx0, tx1, ty0, ty1;
 };
@@ -63,12 +63,12 @@ constexpr int64_t kTemporalSlackRows = 8 * 96;
 // Up to 4 disjoint tile regions in one launch.
 hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, const TileRegion *r, int nreg,
                         int m, Wrap wrap, hipStream_t s);
-int temporal_rows();              // register rows per wave (32/48/64/80/96)
+int temporal_rows(bool bit);      // register rows per wave (32/48/64/80/96)
 // VALU instructions the lanes at one lane position of a tile's waves issue
 // for m generations (the op-count model of life_kernels.hip tstep_kernel,
 // checked against the SQ_INSTS_VALU counter in profiles/); x 64 lanes x tiles.
-double tstep_valu_per_tile_lane(int m);
-void set_temporal_rows(int nr);
+double tstep_valu_per_tile_lane(int m, bool byte);
+void set_temporal_rows(int kernel, int nr);  // kernel -1: both encodings
 
 // LDS-resident path for small single-shard grids: all `gens` generations in
 // one single-workgroup launch (in -> out; in may equal out).  Usable when
@@ -79,9 +79,12 @@ hipError_t launch_small(const life_layout &L, const uint8_t *in, uint8_t *out, i
 
 // Column halo staging: pack writes the last xapron columns to slot 0 and the
 // first xapron columns to slot 1 (h rows each: 1 byte 0/1 per row for a cell
-// column, the dword per row for a bit-encoded word column); unpack writes
+// column, the dword per row for a bit-encoded word column, 32 bytes per row
+// for a byte-encoded word column); unpack writes
 // slot 0 into x in [-xapron, 0) and slot 1 into [w, w + xapron).
-inline int64_t column_bytes_per_row(const life_layout &L) { return L.xapron == 32 ? 4 : 1; }
+inline int64_t column_bytes_per_row(const life_layout &L) {
+    return L.xapron == 32 ? (L.kernel == LIFE_KERNEL_BIT ? 4 : 32) : 1;
+}
 hipError_t launch_pack_columns(const life_layout &L, const uint8_t *buf, uint8_t *stage,
                                hipStream_t s);
 hipError_t launch_unpack_columns(const life_layout &L, uint8_t *buf, const uint8_t *stage,

@@ -344,8 +344,23 @@ __device__ __forceinline__ void bit_hsum(uint32_t v, uint32_t &s0, uint32_t &s1)
     BitEnc::fa(L, v, R, s0, s1);
 }
 
-template <int R, int K, bool WRAPX, bool WRAPY>
-__global__ __launch_bounds__(64 * kStackWaves) void tstep_kernel(TArgs a) {
+// BYTE encoding through the same tiles: a lane's word column is 32 byte cells
+// (two 16-B loads per row), packed into one word on load (v_dot4_u32_u8
+// weights 1..128 per byte pair) and unpacked on store (nibble x 0x204081).
+__device__ __forceinline__ uint32_t pack32(uint4 lo, uint4 hi) {
+    constexpr uint32_t W0 = 0x08040201u, W1 = 0x80402010u;  // bit weights of cells 0-3 / 4-7
+    const uint32_t b3 = __builtin_amdgcn_udot4(hi.z, W0, __builtin_amdgcn_udot4(hi.w, W1, 0u, false), false);
+    const uint32_t b2 = __builtin_amdgcn_udot4(hi.x, W0, __builtin_amdgcn_udot4(hi.y, W1, b3 << 8, false), false);
+    const uint32_t b1 = __builtin_amdgcn_udot4(lo.z, W0, __builtin_amdgcn_udot4(lo.w, W1, b2 << 8, false), false);
+    return __builtin_amdgcn_udot4(lo.x, W0, __builtin_amdgcn_udot4(lo.y, W1, b1 << 8, false), false);
+}
+__device__ __forceinline__ uint32_t unpack_nibble(uint32_t w, int k) {
+    // cells 4k..4k+3 -> bytes 0..3 (bit j of the nibble lands on bit 8j)
+    return __umul24(__builtin_amdgcn_ubfe(w, 4 * k, 4), 0x204081u) & 0x01010101u;
+}
+
+template <bool BYTE, int R, int K, bool WRAPX, bool WRAPY>
+__global__ __launch_bounds__(64 * kStackWaves, 4) void tstep_kernel(TArgs a) {  // 4 waves/SIMD: 2 tiles per CU
     static_assert(R >= 3 && K >= 1 && K <= 32, "window");
     constexpr int NW = kStackWaves;
     constexpr int T = NW * R - 2 * K;
@@ -367,7 +382,7 @@ __global__ __launch_bounds__(64 * kStackWaves) void tstep_kernel(TArgs a) {
     } else {
         jl = j > a.W ? a.W : j;  // words -1 .. W hold cells/apron; beyond: clamp (never stored)
     }
-    const uint32_t voff = (uint32_t)(a.xoff + 4 * jl);
+    const uint32_t voff = (uint32_t)(a.xoff + (BYTE ? 32 : 4) * jl);
     const int64_t y0 = ty * T - K + (int64_t)wi * R;  // owned row of register row 0 (>= -K)
     // Row pointers are walked: with a periodic y axis the walk wraps at h;
     // with an apron the last tile's window may run past the apron row h+K-1
@@ -383,7 +398,12 @@ __global__ __launch_bounds__(64 * kStackWaves) void tstep_kernel(TArgs a) {
     uint32_t v[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        v[r] = *reinterpret_cast<const uint32_t *>(p + voff);
+        if (BYTE) {
+            const uint4 *q = reinterpret_cast<const uint4 *>(p + voff);
+            v[r] = pack32(q[0], q[1]);
+        } else {
+            v[r] = *reinterpret_cast<const uint32_t *>(p + voff);
+        }
         ++y;
         if (WRAPY) {
             if (y == a.h) {
@@ -446,7 +466,17 @@ __global__ __launch_bounds__(64 * kStackWaves) void tstep_kernel(TArgs a) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         if (r < r0 || r >= r1) continue;
-        if (st && y0 + r < a.h) *reinterpret_cast<uint32_t *>(q) = v[r];
+        if (st && y0 + r < a.h) {
+            if (BYTE) {
+                uint4 *o = reinterpret_cast<uint4 *>(q);
+                o[0] = make_uint4(unpack_nibble(v[r], 0), unpack_nibble(v[r], 1), unpack_nibble(v[r], 2),
+                                  unpack_nibble(v[r], 3));
+                o[1] = make_uint4(unpack_nibble(v[r], 4), unpack_nibble(v[r], 5), unpack_nibble(v[r], 6),
+                                  unpack_nibble(v[r], 7));
+            } else {
+                *reinterpret_cast<uint32_t *>(q) = v[r];
+            }
+        }
         q += a.pitch;
     }
 }
@@ -571,10 +601,19 @@ __global__ void pack_columns_kernel(const uint8_t *buf, int64_t pitch, int64_t y
     const int64_t y = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (y >= h) return;
     const uint8_t *row = buf + (y + ya) * pitch;
-    if (xa == 32) {
+    if (xa == 32 && bit) {
         const uint32_t *wd = reinterpret_cast<const uint32_t *>(row + xoff);
         reinterpret_cast<uint32_t *>(stage)[y] = wd[(w - 32) >> 5];
         reinterpret_cast<uint32_t *>(stage)[h + y] = wd[0];
+        return;
+    }
+    if (xa == 32) {  // 32 byte cells per row and side
+        const uint4 *r = reinterpret_cast<const uint4 *>(row + xoff + w - 32), *l = reinterpret_cast<const uint4 *>(row + xoff);
+        uint4 *st = reinterpret_cast<uint4 *>(stage);
+        st[2 * y] = r[0];
+        st[2 * y + 1] = r[1];
+        st[2 * (h + y)] = l[0];
+        st[2 * (h + y) + 1] = l[1];
         return;
     }
     stage[y] = (uint8_t)get_cell(row, xoff, w - 1, bit);
@@ -586,10 +625,19 @@ __global__ void unpack_columns_kernel(uint8_t *buf, int64_t pitch, int64_t ya, i
     const int64_t y = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (y >= h) return;
     uint8_t *row = buf + (y + ya) * pitch;
-    if (xa == 32) {
+    if (xa == 32 && bit) {
         uint32_t *wd = reinterpret_cast<uint32_t *>(row + xoff);
         wd[-1] = reinterpret_cast<const uint32_t *>(stage)[y];
         wd[w >> 5] = reinterpret_cast<const uint32_t *>(stage)[h + y];
+        return;
+    }
+    if (xa == 32) {
+        uint4 *l = reinterpret_cast<uint4 *>(row + xoff - 32), *r = reinterpret_cast<uint4 *>(row + xoff + w);
+        const uint4 *st = reinterpret_cast<const uint4 *>(stage);
+        l[0] = st[2 * y];
+        l[1] = st[2 * y + 1];
+        r[0] = st[2 * (h + y)];
+        r[1] = st[2 * (h + y) + 1];
         return;
     }
     set_cell(row, xoff, -1, stage[y] ? 1u : 0u, bit);
@@ -705,14 +753,17 @@ namespace {
 // byte R64/D2 were the fastest of {16,32,64} x {2,4,8}.
 struct Tunings {
     StepTuning t[2];  // [0] byte, [1] bit
-    int nr = 64;      // temporal stencil: register rows per wave (window = kStackWaves * nr
-                      // rows, tile = window - 2K); fastest measured at 65536^2
+    // temporal stencil: register rows per wave (window = kStackWaves * rows,
+    // tile = window - 2K), per encoding [byte, bit]; fastest measured at
+    // 65536^2 with K = 32 (profiles/r01/tune_*_k32.jsonl)
+    int nr[2] = {48, 96};
     Tunings() : t{{64, 2}, {16, 8}} {
         for (StepTuning &v : t) {
             if (const char *e = getenv("LIFE_STEP_ROWS")) v.rows = atoi(e);
             if (const char *e = getenv("LIFE_STEP_DEPTH")) v.depth = atoi(e);
         }
-        if (const char *e = getenv("LIFE_TEMPORAL_ROWS")) nr = atoi(e);
+        if (const char *e = getenv("LIFE_TEMPORAL_ROWS")) nr[1] = atoi(e);
+        if (const char *e = getenv("LIFE_TEMPORAL_ROWS_BYTE")) nr[0] = atoi(e);
     }
 };
 Tunings &tunings() {
@@ -724,20 +775,22 @@ bool temporal_rows_ok(int nr) { return nr == 32 || nr == 48 || nr == 64 || nr ==
 
 StepTuning step_tuning(bool bit) { return tunings().t[bit ? 1 : 0]; }
 
-int temporal_rows() {
-    const int nr = tunings().nr;
-    return temporal_rows_ok(nr) ? nr : 64;
+int temporal_rows(bool bit) {
+    const int nr = tunings().nr[bit ? 1 : 0];
+    return temporal_rows_ok(nr) ? nr : (bit ? 96 : 48);
 }
 
 // Per register row and generation: bit_hsum = 2 DPP moves + 2 v_alignbit +
 // 2 v_bitop3, rule1 = 8 v_bitop3; kStackWaves waves of temporal_rows() rows
-// per tile.
-double tstep_valu_per_tile_lane(int m) {
-    return 14.0 * (double)kStackWaves * (double)temporal_rows() * (double)m;
+// per tile; the byte encoding adds pack (8 v_dot4 + 3 shifts) and unpack
+// (8 x bfe/mul24/and) once per row and launch.
+double tstep_valu_per_tile_lane(int m, bool byte) {
+    return (double)kStackWaves * (double)temporal_rows(!byte) * (14.0 * (double)m + (byte ? 35.0 : 0.0));
 }
 
-void set_temporal_rows(int nr) {
-    if (temporal_rows_ok(nr)) tunings().nr = nr;
+void set_temporal_rows(int kernel, int nr) {
+    for (int k = 0; k < 2; k++)
+        if ((kernel < 0 || kernel == k) && temporal_rows_ok(nr)) tunings().nr[k] = nr;
 }
 
 void set_step_tuning(int kernel, int rows, int depth) {
@@ -804,28 +857,28 @@ hipError_t launch_step(const life_layout &L, const uint8_t *in, uint8_t *out, ui
 }
 
 namespace {
-template <int R, int K>
+template <bool BYTE, int R, int K>
 hipError_t launch_t(const TArgs &a, Wrap wrap, unsigned grid, hipStream_t s) {
     constexpr unsigned kThreads = 64 * kStackWaves;
     if (wrap.x && wrap.y)
-        tstep_kernel<R, K, true, true><<<grid, kThreads, 0, s>>>(a);
+        tstep_kernel<BYTE, R, K, true, true><<<grid, kThreads, 0, s>>>(a);
     else if (wrap.x)
-        tstep_kernel<R, K, true, false><<<grid, kThreads, 0, s>>>(a);
+        tstep_kernel<BYTE, R, K, true, false><<<grid, kThreads, 0, s>>>(a);
     else if (wrap.y)
-        tstep_kernel<R, K, false, true><<<grid, kThreads, 0, s>>>(a);
+        tstep_kernel<BYTE, R, K, false, true><<<grid, kThreads, 0, s>>>(a);
     else
-        tstep_kernel<R, K, false, false><<<grid, kThreads, 0, s>>>(a);
+        tstep_kernel<BYTE, R, K, false, false><<<grid, kThreads, 0, s>>>(a);
     return hipGetLastError();
 }
 
-template <int K>
+template <bool BYTE, int K>
 hipError_t launch_k(const TArgs &a, Wrap wrap, unsigned grid, hipStream_t s) {
-    switch (temporal_rows()) {
-    case 32: return launch_t<32, K>(a, wrap, grid, s);
-    case 48: return launch_t<48, K>(a, wrap, grid, s);
-    case 80: return launch_t<80, K>(a, wrap, grid, s);
-    case 96: return launch_t<96, K>(a, wrap, grid, s);
-    default: return launch_t<64, K>(a, wrap, grid, s);
+    switch (temporal_rows(!BYTE)) {
+    case 32: return launch_t<BYTE, 32, K>(a, wrap, grid, s);
+    case 48: return launch_t<BYTE, 48, K>(a, wrap, grid, s);
+    case 80: return launch_t<BYTE, 80, K>(a, wrap, grid, s);
+    case 96: return launch_t<BYTE, 96, K>(a, wrap, grid, s);
+    default: return launch_t<BYTE, 64, K>(a, wrap, grid, s);
     }
 }
 }  // namespace
@@ -833,7 +886,7 @@ hipError_t launch_k(const TArgs &a, Wrap wrap, unsigned grid, hipStream_t s) {
 TileGeom tile_geom(const life_layout &L) {
     TileGeom g;
     g.words = 62;
-    g.rows = (int64_t)kStackWaves * temporal_rows() - 2 * (int64_t)L.generations_per_exchange;
+    g.rows = (int64_t)kStackWaves * temporal_rows(is_bit(L)) - 2 * (int64_t)L.generations_per_exchange;
     g.ntx = (L.w / 32 + g.words - 1) / g.words;
     g.nty = (L.h + g.rows - 1) / g.rows;
     return g;
@@ -842,7 +895,8 @@ TileGeom tile_geom(const life_layout &L) {
 hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, const TileRegion *r, int nreg,
                         int m, Wrap wrap, hipStream_t s) {
     const int K = L.generations_per_exchange;
-    if (nreg < 0 || nreg > kMaxRegions || m > K || (K != 8 && K != 16) || L.yapron != K) return hipErrorInvalidValue;
+    if (nreg < 0 || nreg > kMaxRegions || m > K || (K != 8 && K != 16 && K != 32) || L.yapron != K)
+        return hipErrorInvalidValue;
     TArgs a;
     a.in = in;
     a.out = out;
@@ -864,7 +918,11 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
     }
     if (a.nreg == 0 || m <= 0) return hipSuccess;
     const unsigned grid = (unsigned)a.first[a.nreg];  // one workgroup per tile
-    return K == 16 ? launch_k<16>(a, wrap, grid, s) : launch_k<8>(a, wrap, grid, s);
+    if (is_bit(L))
+        return K == 16 ? launch_k<false, 16>(a, wrap, grid, s)
+                       : K == 32 ? launch_k<false, 32>(a, wrap, grid, s) : launch_k<false, 8>(a, wrap, grid, s);
+    return K == 16 ? launch_k<true, 16>(a, wrap, grid, s)
+                   : K == 32 ? launch_k<true, 32>(a, wrap, grid, s) : launch_k<true, 8>(a, wrap, grid, s);
 }
 
 int64_t small_lds_bytes(const life_layout &L) {

@@ -37,23 +37,27 @@ void life_dims_create(int n, int dims[2]) {
     dims[1] = d1;
 }
 
-// Generations per halo exchange of the temporally blocked layout:
-// LIFE_TEMPORAL_DEPTH, or 8 / 16 from the environment variable of the same
-// name (read once; every rank of a job must see the same value).
-static int temporal_depth() {
-    static const int k = [] {
-        const char *e = getenv("LIFE_TEMPORAL_DEPTH");
-        const int v = e ? atoi(e) : 0;
-        return v == 8 || v == 16 ? v : LIFE_TEMPORAL_DEPTH;
-    }();
-    return k;
+// Generations per halo exchange of the temporally blocked layout, per
+// encoding: LIFE_TEMPORAL_DEPTH (bit) / LIFE_TEMPORAL_DEPTH_BYTE, or 8 / 16 /
+// 32 from the environment variables of the same names (read once; every rank
+// of a job must see the same values).  The byte encoding moves 8x the bytes
+// per cell, so it amortises each HBM pass over more generations.
+static int env_depth(const char *name, int dflt) {
+    const char *e = getenv(name);
+    const int v = e ? atoi(e) : 0;
+    return v == 8 || v == 16 || v == 32 ? v : dflt;
+}
+static int temporal_depth(int kernel) {
+    static const int kbit = env_depth("LIFE_TEMPORAL_DEPTH", LIFE_TEMPORAL_DEPTH);
+    static const int kbyte = env_depth("LIFE_TEMPORAL_DEPTH_BYTE", LIFE_TEMPORAL_DEPTH_BYTE);
+    return kernel == LIFE_KERNEL_BIT ? kbit : kbyte;
 }
 
-// The bit-packed temporally blocked stencil exchanges whole 32-cell words
+// The temporally blocked stencil (either encoding) exchanges whole 32-cell words
 // in x and K = temporal_depth() rows in y, and wraps a non-partitioned x axis
 // at word granularity: every block width must be a multiple of 32, and a
 // partitioned y axis needs blocks at least as tall as the apron it feeds.
-static bool temporal_ok(int64_t nx, int64_t ny, int dims0, int dims1) {
+static bool temporal_ok(int64_t nx, int64_t ny, int dims0, int dims1, int K) {
     for (int k = 0; k < dims0; k++) {
         int64_t s, e;
         life_decomposition(nx, dims0, k, &s, &e);
@@ -63,7 +67,7 @@ static bool temporal_ok(int64_t nx, int64_t ny, int dims0, int dims1) {
         for (int k = 0; k < dims1; k++) {
             int64_t s, e;
             life_decomposition(ny, dims1, k, &s, &e);
-            if (e - s < temporal_depth()) return false;
+            if (e - s < K) return false;
         }
     return true;
 }
@@ -86,15 +90,17 @@ int life_layout_query(int64_t nx, int64_t ny, int dims0, int dims1, int rank, in
     out->kernel = kernel;
     out->coords[0] = c0;
     out->coords[1] = c1;
-    const bool temporal = kernel == LIFE_KERNEL_BIT && temporal_ok(nx, ny, dims0, dims1);
+    const int K = temporal_depth(kernel);
+    const bool temporal = temporal_ok(nx, ny, dims0, dims1, K);
     out->xapron = temporal ? 32 : 1;
-    out->yapron = temporal ? temporal_depth() : 1;
-    out->generations_per_exchange = temporal ? temporal_depth() : 1;
+    out->yapron = temporal ? K : 1;
+    out->generations_per_exchange = temporal ? K : 1;
     const int64_t cells_per_unit = kernel == LIFE_KERNEL_BIT ? 128 : 16;
     out->units = (out->w + cells_per_unit - 1) / cells_per_unit;
     out->xoff = kXoff;
-    // room for the last unit, the right apron (cell or word) and the right extra dword
-    out->pitch = round_up(kXoff + 16 * out->units + 16, 256);
+    // room for the last unit, the right apron (cell, word, or 32 byte cells)
+    // and the right extra dword
+    out->pitch = round_up(kXoff + 16 * out->units + (temporal && kernel == LIFE_KERNEL_BYTE ? 32 : 16), 256);
     out->rows = out->h + 2 * out->yapron;
     return LIFE_OK;
 }

@@ -39,7 +39,9 @@ XPORT_AUTO, XPORT_RCCL, XPORT_LOCAL = 0, 1, 2
 HALO_SEND, HALO_RECV, HALO_FILL = 0, 1, 2
 HALO_COLUMN, HALO_ROW = 0, 1
 OPT_SMALL_GRID, OPT_OVERLAP = 1, 2
-TEMPORAL_DEPTH = 16  # LIFE_TEMPORAL_DEPTH: generations per halo exchange of the temporal layout
+# LIFE_TEMPORAL_DEPTH(_BYTE): generations per halo exchange of the temporal layouts
+TEMPORAL_DEPTH = {"bit": 32, "byte": 32}
+TEMPORAL_ROWS = {"bit": 96, "byte": 48}  # default register rows per wave of the temporal tiles
 
 # Every symbol include/life_mi355x.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = (
@@ -116,7 +118,7 @@ def _lib():
         L.life_dev_kernel_stats.argtypes = [vp, P(ctypes.c_double), P(i64), P(ctypes.c_double)]
         L.life_dev_kernel_work.argtypes = [vp, P(ctypes.c_double), P(ctypes.c_double)]
         L.life_tune.argtypes = [i32, i32, i32]
-        L.life_tune_temporal.argtypes = [i32]
+        L.life_tune_temporal.argtypes = [i32, i32]
         L.life_dev_destroy.argtypes = [vp]
         L.life_dev_destroy.restype = None
         _LIB = L
@@ -169,9 +171,10 @@ def density_to_thr(density: float) -> int:
     return min(int(density * 2.0**32), 0xFFFFFFFF)
 
 
-def tune_temporal(rows: int = 0) -> None:
-    """Temporal tile height (registers rows per lane: 48/64/80/96)."""
-    _check(_lib().life_tune_temporal(rows), "life_tune_temporal")
+def tune_temporal(rows: int = 0, kernel=-1) -> None:
+    """Temporal tile height: register rows per wave (32/48/64/80/96) of one
+    encoding, or of both (kernel -1)."""
+    _check(_lib().life_tune_temporal(kernel_id(kernel), rows), "life_tune_temporal")
 
 
 def tune(rows: int = 0, depth: int = 0, kernel=-1) -> None:

@@ -28,13 +28,14 @@ a = p.parse_args()
 
 if a.temporal:
     heights = [int(v) for v in a.temporal.split(",")]
-    life = lm.Life(a.size, a.size, kernel="bit")
+    tk = a.kernels.split(",")[0]
+    life = lm.Life(a.size, a.size, kernel=tk)
     K = life.layout().generations_per_exchange
     life.fill_random(1, 0.5)
     res = {v: [] for v in heights}
     for rnd in range(a.rounds):
         for v in heights:
-            lm.tune_temporal(v)
+            lm.tune_temporal(v, tk)
             life.step(K)
             life.sync()
             life.set_timing(True)
@@ -46,8 +47,9 @@ if a.temporal:
     for v in heights:
         med = statistics.median(m for m, *_ in res[v])
         _, b, upd, valu = res[v][0]
-        print(json.dumps({"kernel": "bit-temporal", "rows_per_wave": v, "K": K, "median_ms_per_launch": round(med, 4),
-                          "gens_per_launch": round(upd / (b / 0.25), 3), "Gcells_per_s": round(upd / med / 1e6, 1),
+        print(json.dumps({"kernel": tk + "-temporal", "rows_per_wave": v, "K": K, "median_ms_per_launch": round(med, 4),
+                          "gens_per_launch": round(upd / (b / (0.25 if tk == "bit" else 2.0)), 3),
+                          "Gcells_per_s": round(upd / med / 1e6, 1),
                           "hbm_GBps": round(b / med / 1e6, 1), "valu_Tops": round(valu / med / 1e9, 2),
                           "live": life.live_count()}), flush=True)
     life.close()

@@ -96,12 +96,13 @@ def _worker(rank, world, port, nx, ny, dims, gens, seed, kernel, q):
 
 @pytest.mark.parametrize("kernel,world,nx,ny,gens", [
     ("byte", 2, 23, 17, 6), ("byte", 4, 20, 9, 7), ("byte", 8, 33, 10, 5), ("byte", 3, 7, 11, 4),
-    ("byte", 8, 4, 2, 3), ("byte", 6, 31, 25, 5),
+    ("byte", 8, 4, 2, 3), ("byte", 6, 31, 25, 5), ("byte", 4, 64, 40, 35), ("byte", 2, 64, 16, 20), ("byte", 4, 64, 80, 70),
     ("bit", 2, 64, 20, 19), ("bit", 4, 64, 16, 17), ("bit", 8, 128, 16, 12), ("bit", 3, 96, 9, 9),
     ("bit", 4, 70, 20, 5), ("bit", 4, 64, 40, 35), ("bit", 8, 128, 36, 20), ("bit", 2, 96, 34, 33),
+    ("bit", 4, 64, 80, 70), ("bit", 8, 128, 64, 40),
 ])
 def test_plan_over_gloo(oracle, lm, kernel, world, nx, ny, gens):
-    """byte: one-cell aprons, one generation per exchange.  bit: 32-cell x /
+    """Either encoding: 32-cell x /
     K-row y aprons, up to K = 16 generations per exchange (temporal layouts),
     or the one-cell fallback when a block width is not a multiple of 32 or a
     partitioned block is shorter than K rows."""

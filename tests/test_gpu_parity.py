@@ -60,8 +60,9 @@ def test_multi_shard_local(gpu, oracle, kernel, shards, dims, nx, ny):
         assert life.live_count() == int(want.sum())
 
 
-def test_byte_equals_bit_long(gpu, oracle):
-    nx, ny, gens = 1024, 768, 200
+@pytest.mark.parametrize("nx", [1024, 1000], ids=["temporal", "onegen"])
+def test_byte_equals_bit_long(gpu, oracle, nx):
+    ny, gens = 768, 200
     g0 = oracle.fill_random(nx, ny, seed=11, density=0.5)
     out = {}
     for k in ("byte", "bit"):
@@ -73,8 +74,8 @@ def test_byte_equals_bit_long(gpu, oracle):
     np.testing.assert_array_equal(out["bit"], oracle.life_run(g0, gens, threads=4))
 
 
-@pytest.mark.parametrize("kernel,nx,launches,gens", [("bit", 4096, 2, 20), ("bit", 4016, 13, 13),
-                                                     ("byte", 4096, 13, 13)])
+@pytest.mark.parametrize("kernel,nx,launches,gens", [("bit", 4096, 2, 40), ("bit", 4016, 13, 13),
+                                                     ("byte", 4096, 2, 40), ("byte", 4016, 13, 13)])
 def test_timing_stats(gpu, kernel, nx, launches, gens):
     """One timed launch per generation (one-generation kernels) or per up to
     8 generations (temporal bit kernel).  Bytes are the compulsory HBM
@@ -92,19 +93,24 @@ def test_timing_stats(gpu, kernel, nx, launches, gens):
         assert n * upd == pytest.approx(nx * 4096 * gens)
         temporal = launches < gens
         assert (valu > 0) == temporal
-        if temporal:  # 3 x 9 tiles of 62 words x 480 rows (8 waves x 64 rows - 2K), 64 lanes
-            assert n * valu == pytest.approx(3 * 9 * 64 * 14 * 8 * 64 * gens)
+        if temporal:  # 3 x ceil(4096 / (8 waves x R rows - 2K)) tiles of 62 words, 64 lanes;
+            # byte: + pack/unpack (35 ops per register row per launch)
+            R, K = gpu.TEMPORAL_ROWS[kernel], gpu.TEMPORAL_DEPTH[kernel]
+            tiles = 3 * -(-4096 // (8 * R - 2 * K))
+            per_row = 14 * gens + (35 * launches if kernel == "byte" else 0)
+            assert n * valu == pytest.approx(tiles * 64 * 8 * R * per_row)
 
 
 # ---------------------------------------------------------------- temporal blocking (bit)
+@pytest.mark.parametrize("kernel", ["bit", "byte"])
 @pytest.mark.parametrize("nx,ny", [(32, 1), (32, 5), (64, 64), (96, 33), (2048, 100), (1024, 1000), (4096, 48),
                                    (32, 200), (1984, 130), (2016, 7)])
-def test_temporal_single_shard(gpu, oracle, nx, ny):
+def test_temporal_single_shard(gpu, oracle, kernel, nx, ny):
     """Word-aligned widths take the temporally blocked kernel (up to K = 16
     generations per launch); runs of 1, 7, 8, 9, 20 and 40 generations."""
-    assert gpu.layout_query(nx, ny, (1, 1), 0, "bit").generations_per_exchange == gpu.TEMPORAL_DEPTH
+    assert gpu.layout_query(nx, ny, (1, 1), 0, kernel).generations_per_exchange == gpu.TEMPORAL_DEPTH[kernel]
     g0 = oracle.fill_random(nx, ny, seed=nx + 3 * ny, density=0.5)
-    with gpu.Life(nx, ny, kernel="bit", small_grid=False) as life:
+    with gpu.Life(nx, ny, kernel=kernel, small_grid=False) as life:
         life.upload(g0)
         done = 0
         for n in (1, 7, 8, 9, 20, 40):
@@ -118,34 +124,38 @@ def test_temporal_single_shard(gpu, oracle, nx, ny):
     (256, 64, 4, (2, 2)), (512, 80, 8, (4, 2)), (64, 80, 4, (1, 4)), (256, 9, 4, (4, 1)), (64, 20, 2, (2, 1)),
     (96, 32, 6, (3, 2)), (4096, 4096, 4, (2, 2)), (8192, 200, 8, (4, 2)), (2048, 1100, 2, (1, 2)),
 ])
-def test_temporal_multi_shard_local(gpu, oracle, nx, ny, shards, dims):
+@pytest.mark.parametrize("kernel", ["bit", "byte"])
+def test_temporal_multi_shard_local(gpu, oracle, kernel, nx, ny, shards, dims):
     """K-deep aprons through the LOCAL transport: whole-word columns, K-row
     blocks of rows, ring tiles first, interior overlapped with the exchange."""
     for r in range(shards):
-        assert gpu.layout_query(nx, ny, dims, r, "bit").generations_per_exchange == gpu.TEMPORAL_DEPTH
+        K = gpu.TEMPORAL_DEPTH[kernel]  # a partitioned block shorter than K rows takes the one-cell path
+        want = K if dims[1] == 1 or ny // dims[1] >= K else 1
+        assert gpu.layout_query(nx, ny, dims, r, kernel).generations_per_exchange == want
     g0 = oracle.fill_random(nx, ny, seed=7 * shards + ny, density=0.45)
-    with gpu.Life(nx, ny, shards=shards, kernel="bit", dims=dims, transport=gpu.XPORT_LOCAL) as life:
+    with gpu.Life(nx, ny, shards=shards, kernel=kernel, dims=dims, transport=gpu.XPORT_LOCAL) as life:
         life.upload(g0)
         done = 0
-        for n in (1, 8, 13, 16, 30):
+        for n in (1, 8, 13, 16, 30, 40):
             life.step(n)
             done += n
             np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, done, threads=4),
                                           err_msg=f"after {done} generations")
 
 
+@pytest.mark.parametrize("kernel", ["bit", "byte"])
 @pytest.mark.parametrize("rows", [32, 48, 64, 80, 96])
-def test_temporal_tile_heights_agree(gpu, oracle, rows):
+def test_temporal_tile_heights_agree(gpu, oracle, kernel, rows):
     nx, ny = 2048, 333
     g0 = oracle.fill_random(nx, ny, seed=rows, density=0.5)
-    gpu.tune_temporal(rows)
+    gpu.tune_temporal(rows, kernel)
     try:
-        with gpu.Life(nx, ny, kernel="bit", small_grid=False) as life:
+        with gpu.Life(nx, ny, kernel=kernel, small_grid=False) as life:
             life.upload(g0)
-            life.step(29)
-            np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, 29, threads=4))
+            life.step(40)
+            np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, 40, threads=4))
     finally:
-        gpu.tune_temporal(64)
+        gpu.tune_temporal(gpu.TEMPORAL_ROWS[kernel], kernel)
 
 
 # ---------------------------------------------------------------- LDS-resident small grids

@@ -137,14 +137,18 @@ def test_halo_plan_is_symmetric(lm, kernel, nx, ny, dims):
 
 @pytest.mark.parametrize("nx,ny,dims,temporal", [(65536, 65536, (1, 1), True), (262144, 131072, (4, 2), True),
                                                  (1000, 37, (1, 1), False), (64, 7, (2, 1), True),
-                                                 (64, 14, (1, 2), False), (96, 32, (3, 2), True),
-                                                 (96, 30, (3, 2), False)])
+                                                 (64, 14, (1, 2), False), (96, 64, (3, 2), True),
+                                                 (96, 62, (3, 2), False)])
 def test_temporal_mode_selection(lm, nx, ny, dims, temporal):
     for r in range(dims[0] * dims[1]):
         L = lm.layout_query(nx, ny, dims, r, "bit")
-        K = lm.TEMPORAL_DEPTH
+        K = lm.TEMPORAL_DEPTH["bit"]
         assert (L.generations_per_exchange == K) == temporal
         assert (L.xapron, L.yapron) == ((32, K) if temporal else (1, 1))
         assert L.rows == L.h + 2 * L.yapron
-        B = lm.layout_query(nx, ny, dims, r, "byte")
-        assert (B.xapron, B.yapron, B.generations_per_exchange) == (1, 1, 1)
+        B = lm.layout_query(nx, ny, dims, r, "byte")  # the byte encoding takes the same tiles, K = 32
+        KB = lm.TEMPORAL_DEPTH["byte"]
+        tb = temporal and (dims[1] == 1 or ny // dims[1] >= KB)
+        assert (B.xapron, B.yapron, B.generations_per_exchange) == ((32, KB, KB) if tb else (1, 1, 1))
+        if tb:  # room for the 32-byte right apron
+            assert B.pitch >= B.xoff + B.w + 32
