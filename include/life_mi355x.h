@@ -162,6 +162,13 @@ int life_dev_gather(life_dev *d, uint8_t *grid);
 /* Live cells over the whole grid (all ranks). Blocking. */
 int64_t life_dev_live_count(life_dev *d);
 
+/* Position-weighted checksum of the whole grid (all ranks), independent of
+ * the encoding and the partition: sum over live cells (x, y) of
+ * mix64(y*nx + x + 1) mod 2^64, mix64(v) = t ^ (t >> 29), t = v *
+ * 0x9E3779B97F4A7C15 mod 2^64.  Lets N-shard and 1-shard runs of one grid be
+ * compared at sizes no host gather reaches.  Blocking. */
+int life_dev_checksum(life_dev *d, uint64_t *sum);
+
 int life_dev_sync(life_dev *d);
 int life_dev_layout(life_dev *d, int local_shard, life_layout *out);
 int life_dev_world(life_dev *d, int *world, int *dims0, int *dims1, int *nlocal, int *transport);

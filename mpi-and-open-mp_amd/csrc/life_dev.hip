@@ -75,10 +75,11 @@ struct Shard {
     hipStream_t stream2 = nullptr;  // compute: interior, concurrent with ring + halo
     hipStream_t comm_stream = nullptr;
     hipEvent_t ev_ring = nullptr, ev_halo = nullptr, ev_sync = nullptr, ev_int = nullptr, ev_join = nullptr;
+    hipEvent_t ev_entry = nullptr;  // life_dev_step entry fence (see there)
     ncclComm_t comm = nullptr;
     uint8_t *col_send = nullptr, *col_recv = nullptr;  // 2*h bytes each
-    unsigned long long *d_count = nullptr;
-    unsigned long long *h_count = nullptr;  // pinned
+    unsigned long long *d_count = nullptr;  // census: live count, checksum
+    unsigned long long *h_count = nullptr;  // pinned, 2 entries
     uint8_t *sink = nullptr;  // stencil stores of lanes outside a region
     std::vector<life_halo_op> plan;
     std::vector<TimedLaunch> timers;
@@ -125,12 +126,13 @@ int shard_alloc(life_dev *d, Shard &s) {
     HIPCHK(hipEventCreateWithFlags(&s.ev_ring, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&s.ev_halo, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&s.ev_sync, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&s.ev_entry, hipEventDisableTiming));
     const size_t col_bytes = (size_t)(2 * s.lay.h * life::column_bytes_per_row(s.lay));
     HIPCHK(hipMalloc(&s.col_send, col_bytes));
     HIPCHK(hipMalloc(&s.col_recv, col_bytes));
-    HIPCHK(hipMalloc(&s.d_count, sizeof(unsigned long long)));
+    HIPCHK(hipMalloc(&s.d_count, 2 * sizeof(unsigned long long)));
     HIPCHK(hipMalloc(&s.sink, 1024));
-    HIPCHK(hipHostMalloc(&s.h_count, sizeof *s.h_count, hipHostMallocDefault));
+    HIPCHK(hipHostMalloc(&s.h_count, 2 * sizeof *s.h_count, hipHostMallocDefault));
     life_halo_op ops[16];
     const int n = life_halo_plan(d->nx, d->ny, d->dims[0], d->dims[1], s.rank, d->kernel, ops, 16);
     if (n < 0) {
@@ -152,7 +154,7 @@ void shard_free(Shard &s) {
         if (p) (void)hipFree(p);
     if (s.d_count) (void)hipFree(s.d_count);
     if (s.h_count) (void)hipHostFree(s.h_count);
-    for (hipEvent_t e : {s.ev_ring, s.ev_halo, s.ev_sync, s.ev_int, s.ev_join})
+    for (hipEvent_t e : {s.ev_ring, s.ev_halo, s.ev_sync, s.ev_int, s.ev_join, s.ev_entry})
         if (e) (void)hipEventDestroy(e);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     if (s.stream2) (void)hipStreamDestroy(s.stream2);
@@ -688,6 +690,16 @@ static int step_small(life_dev *d, int64_t generations) {
 int life_dev_step(life_dev *d, int64_t generations) {
     if (!d || generations < 0) return LIFE_EINVAL;
     if (generations == 0) return LIFE_OK;
+    // Entry fence: the second compute stream and the comm stream start after
+    // everything already queued on the compute stream (an asynchronous
+    // fill_random and its halo fill, a small-grid launch, a gather's export),
+    // which the overlapped schedule would otherwise race.
+    for (Shard &s : d->shards) {
+        HIPCHK(hipSetDevice(s.device));
+        HIPCHK(hipEventRecord(s.ev_entry, s.stream));
+        HIPCHK(hipStreamWaitEvent(s.stream2, s.ev_entry, 0));
+        HIPCHK(hipStreamWaitEvent(s.comm_stream, s.ev_entry, 0));
+    }
     if (small_grid(d)) {
         constexpr int64_t kChunk = 1 << 20;  // generations per resident launch
         for (int64_t g = 0; g < generations; g += kChunk)
@@ -773,20 +785,37 @@ int life_dev_gather(life_dev *d, uint8_t *grid) {
     return rc;
 }
 
-int64_t life_dev_live_count(life_dev *d) {
-    if (!d) return LIFE_EINVAL;
-    int64_t total = 0;
+static int census(life_dev *d, unsigned long long out[2]) {
+    out[0] = out[1] = 0;
     for (Shard &s : d->shards) {
         HIPCHK(hipSetDevice(s.device));
-        HIPCHK(hipMemsetAsync(s.d_count, 0, sizeof(unsigned long long), s.stream));
-        HIPCHK(life::launch_live_count(s.lay, s.buf[s.cur], s.d_count, s.stream));
+        HIPCHK(hipMemsetAsync(s.d_count, 0, 2 * sizeof(unsigned long long), s.stream));
+        HIPCHK(life::launch_census(s.lay, d->nx, s.buf[s.cur], s.d_count, s.stream));
         if (d->rank_mode && d->world > 1)
-            NCCLCHK(ncclAllReduce(s.d_count, s.d_count, 1, ncclUint64, ncclSum, s.comm, s.stream));
-        HIPCHK(hipMemcpyAsync(s.h_count, s.d_count, sizeof *s.h_count, hipMemcpyDeviceToHost, s.stream));
+            NCCLCHK(ncclAllReduce(s.d_count, s.d_count, 2, ncclUint64, ncclSum, s.comm, s.stream));
+        HIPCHK(hipMemcpyAsync(s.h_count, s.d_count, 2 * sizeof *s.h_count, hipMemcpyDeviceToHost, s.stream));
         HIPCHK(hipStreamSynchronize(s.stream));  // pinned destination
-        total += (int64_t)*s.h_count;
+        out[0] += s.h_count[0];
+        out[1] += s.h_count[1];
     }
-    return total;
+    return LIFE_OK;
+}
+
+int64_t life_dev_live_count(life_dev *d) {
+    if (!d) return LIFE_EINVAL;
+    CHK(life_dev_sync(d));
+    unsigned long long c[2];
+    CHK(census(d, c));
+    return (int64_t)c[0];
+}
+
+int life_dev_checksum(life_dev *d, uint64_t *sum) {
+    if (!d || !sum) return LIFE_EINVAL;
+    CHK(life_dev_sync(d));
+    unsigned long long c[2];
+    CHK(census(d, c));
+    *sum = (uint64_t)c[1];
+    return LIFE_OK;
 }
 
 int life_dev_layout(life_dev *d, int local_shard, life_layout *out) {

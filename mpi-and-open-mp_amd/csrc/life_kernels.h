@@ -100,8 +100,9 @@ hipError_t launch_export_block(const life_layout &L, const uint8_t *buf, uint8_t
 hipError_t launch_fill_random(const life_layout &L, int64_t nx, uint64_t key, uint32_t thr32,
                               uint8_t *buf, hipStream_t s);
 
-// Adds the number of live owned cells to *count.
-hipError_t launch_live_count(const life_layout &L, const uint8_t *buf,
-                             unsigned long long *count, hipStream_t s);
+// Adds the live owned cells' count to out[0] and their checksum
+// (sum of mix64(global y*nx + x + 1), mod 2^64) to out[1].
+hipError_t launch_census(const life_layout &L, int64_t nx, const uint8_t *buf, unsigned long long *out,
+                         hipStream_t s);
 
 }  // namespace life

@@ -715,32 +715,56 @@ __global__ void fill_random_kernel(uint8_t *buf, int64_t pitch, int64_t ya, int6
         make_uint4(word[0], word[1], word[2], word[3]);
 }
 
+// Census of the owned cells: live count and the position-weighted checksum
+// sum over live (x, y) of mix64(y*nx + x + 1), both mod 2^64 -- independent
+// of the cell encoding and of the partition, so the 1-GPU and N-shard runs of
+// one grid, and the byte and bit kernels, can be compared at sizes no host
+// copy or CPU oracle reaches.  2-D grid: x over 16-B units, y strides rows.
+__device__ __forceinline__ uint64_t cell_mix(uint64_t v) {
+    v *= 0x9E3779B97F4A7C15ull;
+    return v ^ (v >> 29);
+}
+
 template <int CPU>
-__global__ void live_count_kernel(const uint8_t *buf, int64_t pitch, int64_t ya, int64_t xoff, int64_t w, int64_t h,
-                                  int64_t units, unsigned long long *count) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    unsigned long long c = 0;
-    if (i < units * h) {
-        const int64_t u = i % units, y = i / units;
-        const uint4 q = *reinterpret_cast<const uint4 *>(buf + (y + ya) * pitch + xoff + 16 * u);
-        const uint32_t word[4] = {q.x, q.y, q.z, q.w};
+__global__ void census_kernel(const uint8_t *buf, int64_t pitch, int64_t ya, int64_t xoff, int64_t w, int64_t h,
+                              int64_t units, int64_t gx0, int64_t gy0, int64_t nx, unsigned long long *out) {
+    const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long c = 0, sum = 0;
+    constexpr int kPerWord = CPU / 4;  // cells per dword
+    if (u < units) {
         const int64_t valid = w - u * CPU;  // cells of this unit inside the block
-        constexpr int kPerWord = CPU / 4;
+        uint32_t m[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int64_t left = valid - k * kPerWord;
-            uint32_t m;
-            if (left <= 0)
-                m = 0u;
-            else if (left >= kPerWord)
-                m = 0xFFFFFFFFu;
-            else
-                m = CPU == 16 ? (0xFFFFFFFFu >> (32 - 8 * left)) : (0xFFFFFFFFu >> (32 - left));
-            c += __popc(word[k] & m);  // byte cells are 0/1: popcount == sum
+            m[k] = left <= 0 ? 0u
+                   : left >= kPerWord ? 0xFFFFFFFFu
+                   : (CPU == 16 ? (0xFFFFFFFFu >> (32 - 8 * left)) : (0xFFFFFFFFu >> (32 - left)));
+        }
+        for (int64_t y = blockIdx.y; y < h; y += gridDim.y) {
+            const uint4 q = *reinterpret_cast<const uint4 *>(buf + (y + ya) * pitch + xoff + 16 * u);
+            const uint32_t word[4] = {q.x, q.y, q.z, q.w};
+            const uint64_t base = (uint64_t)((gy0 + y) * nx + gx0 + u * CPU) + 1u;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                uint32_t bits = word[k] & m[k];  // byte cells are 0/1: bit 8j = cell j of the dword
+                c += __popc(bits);
+                while (bits) {
+                    const int b = __ffs(bits) - 1;
+                    bits &= bits - 1u;
+                    sum += cell_mix(base + (uint64_t)(k * kPerWord + (CPU == 16 ? b >> 3 : b)));
+                }
+            }
         }
     }
-    for (int s = 32; s > 0; s >>= 1) c += __shfl_xor(c, s);
-    if ((threadIdx.x & 63) == 0 && c) atomicAdd(count, c);
+    for (int s = 32; s > 0; s >>= 1) {
+        c += __shfl_xor(c, s);
+        sum += __shfl_xor(sum, s);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (c) atomicAdd(out, c);
+        if (sum) atomicAdd(out + 1, sum);
+    }
 }
 
 inline bool is_bit(const life_layout &L) { return L.kernel == LIFE_KERNEL_BIT; }
@@ -997,13 +1021,15 @@ hipError_t launch_fill_random(const life_layout &L, int64_t nx, uint64_t key, ui
     return hipGetLastError();
 }
 
-hipError_t launch_live_count(const life_layout &L, const uint8_t *buf, unsigned long long *count,
-                             hipStream_t s) {
-    const unsigned g = blocks_for(L.units * L.h, 256);
+hipError_t launch_census(const life_layout &L, int64_t nx, const uint8_t *buf, unsigned long long *out,
+                         hipStream_t s) {
+    const dim3 grid(blocks_for(L.units, 256), (unsigned)(L.h < 4096 ? L.h : 4096));
     if (is_bit(L))
-        live_count_kernel<128><<<g, 256, 0, s>>>(buf, L.pitch, L.yapron, L.xoff, L.w, L.h, L.units, count);
+        census_kernel<128><<<grid, 256, 0, s>>>(buf, L.pitch, L.yapron, L.xoff, L.w, L.h, L.units, L.x0, L.y0, nx,
+                                                 out);
     else
-        live_count_kernel<16><<<g, 256, 0, s>>>(buf, L.pitch, L.yapron, L.xoff, L.w, L.h, L.units, count);
+        census_kernel<16><<<grid, 256, 0, s>>>(buf, L.pitch, L.yapron, L.xoff, L.w, L.h, L.units, L.x0, L.y0, nx,
+                                                out);
     return hipGetLastError();
 }
 

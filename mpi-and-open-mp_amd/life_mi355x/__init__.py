@@ -50,7 +50,8 @@ ABI_SYMBOLS = (
     "life_get_unique_id", "life_dev_create_rank", "life_dev_upload", "life_dev_fill_random",
     "life_dev_step", "life_dev_gather", "life_dev_live_count", "life_dev_sync",
     "life_dev_layout", "life_dev_world", "life_dev_set_timing", "life_dev_kernel_stats",
-    "life_tune", "life_tune_temporal", "life_dev_configure", "life_dev_kernel_work", "life_dev_destroy",
+    "life_tune", "life_tune_temporal", "life_dev_configure", "life_dev_kernel_work", "life_dev_checksum",
+    "life_dev_destroy",
 )
 
 
@@ -111,6 +112,7 @@ def _lib():
         L.life_dev_live_count.argtypes = [vp]
         L.life_dev_live_count.restype = i64
         L.life_dev_sync.argtypes = [vp]
+        L.life_dev_checksum.argtypes = [vp, P(ctypes.c_uint64)]
         L.life_dev_layout.argtypes = [vp, i32, P(Layout)]
         L.life_dev_world.argtypes = [vp] + [P(ctypes.c_int)] * 5
         L.life_dev_set_timing.argtypes = [vp, i32]
@@ -244,6 +246,12 @@ class Life:
 
     def live_count(self) -> int:
         return _check(_lib().life_dev_live_count(self._h), "live_count")
+
+    def checksum(self) -> int:
+        """life_dev_checksum: encoding- and partition-independent grid hash."""
+        v = ctypes.c_uint64()
+        _check(_lib().life_dev_checksum(self._h, ctypes.byref(v)), "checksum")
+        return v.value
 
     def sync(self) -> None:
         _check(_lib().life_dev_sync(self._h), "sync")

@@ -143,6 +143,19 @@ def np_life_step(grid: np.ndarray) -> np.ndarray:
     return (born | survive).astype(np.uint8)
 
 
+def checksum(grid: np.ndarray, x0: int = 0, y0: int = 0, nx: int | None = None) -> int:
+    """The definition life_dev_checksum implements (include/life_mi355x.h):
+    sum over live cells of mix64(y*nx + x + 1) mod 2^64 (numpy uint64 wraps)."""
+    ny_, nx_ = grid.shape
+    nx = nx_ if nx is None else nx
+    ys, xs = np.nonzero(grid)
+    v = ((ys.astype(np.uint64) + np.uint64(y0)) * np.uint64(nx) + xs.astype(np.uint64) + np.uint64(x0)
+         + np.uint64(1))
+    with np.errstate(over="ignore"):
+        t = v * np.uint64(0x9E3779B97F4A7C15)
+    return int(np.sum(t ^ (t >> np.uint64(29)), dtype=np.uint64))
+
+
 # ---------------------------------------------------------------- reference (pinning)
 def ref_life_run(grid: np.ndarray, gens: int) -> np.ndarray:
     """The reference's own life_step (3-life/life2d.c:104-130), gens times."""

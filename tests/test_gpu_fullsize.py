@@ -1,0 +1,116 @@
+"""Parity at BASELINE.json's full sizes, where a CPU
+oracle run or a host gather of every case is too slow: size-independent
+properties through the C ABI.
+
+* the census checksum (life_dev_checksum: sum of mix64(global index) over
+  live cells, encoding- and partition-independent) is itself pinned to
+  oracle.checksum on grids the oracle can hold;
+* C3 (random 50% 32768^2, seeds 1-3, 1000 generations): byte kernel == bit
+  kernel; seed 1 also bit-exact against the CPU oracle after 10 generations
+  (full 1 Gcell compare);
+* C4 (random 65536^2, dims {2,1},{2,2},{4,2}): the partitioned run (LOCAL
+  transport: the same plan, pack/unpack and ring/interior schedule as RCCL)
+  == the 1-shard run, by checksum and live count, plus one full compare;
+* C5 (weak scaling, 65536^2 per shard, 8 shards = 262144 x 131072): the
+  8-shard run == the single-block run of the same global grid.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _threads():
+    import os
+
+    return int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+
+
+@pytest.mark.parametrize("kernel", ["bit", "byte"])
+@pytest.mark.parametrize("nx,ny,shards,gens", [(257, 131, 1, 5), (1024, 512, 1, 40), (640, 480, 4, 37),
+                                               (4096, 300, 8, 33), (33, 1, 1, 3)])
+def test_checksum_matches_oracle(gpu, oracle, kernel, nx, ny, shards, gens):
+    g0 = oracle.fill_random(nx, ny, seed=nx + ny, density=0.5)
+    want = oracle.life_run(g0, gens, threads=4)
+    with gpu.Life(nx, ny, shards=shards, kernel=kernel, transport=gpu.XPORT_LOCAL) as life:
+        life.upload(g0)
+        assert life.checksum() == oracle.checksum(g0)
+        life.step(gens)
+        assert life.checksum() == oracle.checksum(want)
+        assert life.live_count() == int(want.sum())
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_c3_byte_equals_bit_32768(gpu, seed):
+    n, gens = 32768, 1000
+    out = {}
+    for kernel in ("bit", "byte"):
+        with gpu.Life(n, n, kernel=kernel) as life:
+            life.fill_random(seed, 0.5)
+            life.step(gens)
+            out[kernel] = (life.checksum(), life.live_count())
+    assert out["bit"] == out["byte"]
+    assert 0 < out["bit"][1] < n * n // 4
+
+
+def test_c3_vs_oracle_32768(gpu, oracle):
+    """Full 1 Gcell grids, 10 generations: GPU (bit and byte) == CPU oracle."""
+    n, gens = 32768, 10
+    with gpu.Life(n, n, kernel="bit") as life:
+        life.fill_random(1, 0.5)
+        g0 = life.gather()
+        life.step(gens)
+        got_bit = life.gather()
+        ck = life.checksum()
+    want = oracle.life_run(g0, gens, threads=_threads())
+    assert np.array_equal(got_bit, want)
+    assert ck == oracle.checksum(want)
+    del got_bit
+    with gpu.Life(n, n, kernel="byte") as life:
+        life.upload(g0)
+        life.step(gens)
+        assert np.array_equal(life.gather(), want)
+
+
+@pytest.mark.parametrize("kernel", ["bit", "byte"])
+@pytest.mark.parametrize("dims", [(2, 1), (2, 2), (4, 2)])
+def test_c4_partitioned_equals_single_65536(gpu, kernel, dims):
+    n, gens = 65536, 70  # two full K = 32 exchanges + a partial one
+    with gpu.Life(n, n, kernel=kernel) as life:
+        life.fill_random(1, 0.5)
+        life.step(gens)
+        want = (life.checksum(), life.live_count())
+    with gpu.Life(n, n, shards=dims[0] * dims[1], kernel=kernel, dims=dims, transport=gpu.XPORT_LOCAL) as life:
+        life.fill_random(1, 0.5)
+        life.step(gens)
+        assert (life.checksum(), life.live_count()) == want
+
+
+def test_c4_full_compare_at_root_65536(gpu):
+    """One case compared cell by cell after the device-side gather."""
+    n, gens = 65536, 40
+    with gpu.Life(n, n, kernel="bit") as life:
+        life.fill_random(2, 0.5)
+        life.step(gens)
+        want = life.gather()
+    with gpu.Life(n, n, shards=8, kernel="bit", transport=gpu.XPORT_LOCAL) as life:
+        life.fill_random(2, 0.5)
+        life.step(gens)
+        assert np.array_equal(life.gather(), want)
+
+
+def test_c5_weak_scaling_shape_8_shards(gpu):
+    """configs[4] at 8 GPUs: 65536^2 per shard, global 262144 x 131072."""
+    dims = gpu.dims_create(8)
+    nx, ny, gens = 65536 * dims[0], 65536 * dims[1], 40
+    with gpu.Life(nx, ny, shards=8, kernel="bit", transport=gpu.XPORT_LOCAL) as life:
+        for r in range(8):
+            L = life.layout(r)
+            assert (L.w, L.h) == (65536, 65536)
+        life.fill_random(3, 0.5)
+        life.step(gens)
+        got = (life.checksum(), life.live_count())
+    with gpu.Life(nx, ny, kernel="bit") as life:
+        life.fill_random(3, 0.5)
+        life.step(gens)
+        assert (life.checksum(), life.live_count()) == got

@@ -184,3 +184,18 @@ def test_repeated_gather_is_stable(gpu, oracle, kernel):
         life.fill_random(1, 0.5)
         for _ in range(6):
             np.testing.assert_array_equal(life.gather(), want)
+
+
+@pytest.mark.parametrize("kernel", ["bit", "byte"])
+def test_step_right_after_async_fill(gpu, oracle, kernel):
+    """fill_random is asynchronous on the compute stream; the overlapped
+    schedule's interior (second stream) and halo (comm stream) must still see
+    the filled grid (life_dev_step's entry fence).  Tall partitioned shards make
+    the fill long enough to race without it."""
+    nx, ny, gens = 4096, 16384, 33
+    with gpu.Life(nx, ny, shards=2, kernel=kernel, dims=(2, 1), transport=gpu.XPORT_LOCAL) as life:
+        life.fill_random(9, 0.5)
+        life.step(gens)
+        got = life.checksum()
+    want = oracle.life_run(oracle.fill_random(nx, ny, 9, 0.5), gens, threads=8)
+    assert got == oracle.checksum(want)

@@ -86,3 +86,25 @@ def test_oracle_vs_linked_reference_life_step(oracle):
     for nx, ny in [(1, 1), (1, 9), (2, 2), (5, 3), (64, 64), (97, 31)]:
         g = oracle.fill_random(nx, ny, nx + ny, 0.45)
         np.testing.assert_array_equal(oracle.ref_life_run(g, 9), oracle.life_run(g, 9))
+
+
+def test_checksum_definition(oracle):
+    """oracle.checksum is the documented life_dev_checksum: one live cell at
+    (x, y) contributes mix64(y*nx + x + 1); contributions add mod 2^64."""
+    def mix(v):
+        t = (v * 0x9E3779B97F4A7C15) % 2**64
+        return t ^ (t >> 29)
+
+    g = np.zeros((7, 11), np.uint8)
+    assert oracle.checksum(g) == 0
+    g[3, 5] = 1
+    assert oracle.checksum(g) == mix(3 * 11 + 5 + 1)
+    g[6, 10] = 1
+    assert oracle.checksum(g) == (mix(3 * 11 + 5 + 1) + mix(6 * 11 + 10 + 1)) % 2**64
+    big = oracle.fill_random(300, 200, 5, 0.5)
+    ys, xs = np.nonzero(big)
+    assert oracle.checksum(big) == sum(mix(int(y) * 300 + int(x) + 1) for y, x in zip(ys, xs)) % 2**64
+    # block form (a shard's owned cells at global origin x0, y0) sums to the whole
+    parts = sum(oracle.checksum(big[y0:y0 + 100, x0:x0 + 150], x0, y0, 300)
+                for y0 in (0, 100) for x0 in (0, 150)) % 2**64
+    assert parts == oracle.checksum(big)
