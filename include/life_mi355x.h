@@ -206,7 +206,7 @@ int life_tune(int kernel, int rows, int depth);
 /* Temporal (generations_per_exchange = K > 1) tile height of encoding
  * `kernel` (-1: both): register rows per wave, 32/48/64/80/96; a tile is one
  * workgroup of 8 vertically stacked waves, 8*rows - 2K owned rows; 0 keeps
- * the current values (defaults bit 96, byte 48, by measurement);
+ * the current values (defaults bit 48, byte 32, by measurement);
  * LIFE_TEMPORAL_ROWS / LIFE_TEMPORAL_ROWS_BYTE override at load time. */
 int life_tune_temporal(int kernel, int rows);
 

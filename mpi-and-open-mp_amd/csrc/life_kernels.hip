@@ -318,7 +318,10 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs a) {
 // (horizontal neighbours) + 10 v_bitop3 (full adder 2, rule 8);
 // scripts/ubench_row.hip prices the row at ~20.7 ns per SIMD at 16 waves/CU.
 constexpr int kMaxRegions = 4;
-constexpr int kStackWaves = 8;  // waves per workgroup (2 per SIMD)
+#ifndef LIFE_STACK_WAVES
+#define LIFE_STACK_WAVES 8
+#endif
+constexpr int kStackWaves = LIFE_STACK_WAVES;  // waves per workgroup (2 per SIMD)
 struct TArgs {
     const uint8_t *in;
     uint8_t *out;
@@ -338,9 +341,31 @@ __device__ __forceinline__ uint32_t right_or_zero(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xf, 0xf, true);
 }
 
+// Where the neighbour words come from (build-time switch): 0: both DPP moves
+// (VALU); 1: both ds_bpermute (LDS pipe); 2 (default): DPP left, ds_bpermute
+// right -- the row is VALU-issue bound, and moving one of its 14 VALU
+// instructions to the otherwise idle LDS pipe measured +10 % (bit, K = 32:
+// 91.0 -> 99.8 Tcell/s at 65536^2; mode 1 lost 13 %: profiles/r01/hsum_modes.txt).
+#ifndef LIFE_HSUM_MODE
+#define LIFE_HSUM_MODE 2
+#endif
+__device__ __forceinline__ uint32_t bperm(int addr, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)v);
+}
 __device__ __forceinline__ void bit_hsum(uint32_t v, uint32_t &s0, uint32_t &s1) {
-    const uint32_t L = __builtin_amdgcn_alignbit(v, left_or_zero(v), 31);
-    const uint32_t R = __builtin_amdgcn_alignbit(right_or_zero(v), v, 1);
+#if LIFE_HSUM_MODE == 0
+    const uint32_t l = left_or_zero(v), r = right_or_zero(v);
+#else
+    const int lane = (int)__lane_id();
+    const uint32_t r = bperm(((lane + 1) & 63) << 2, v);
+#if LIFE_HSUM_MODE == 1
+    const uint32_t l = bperm(((lane - 1) & 63) << 2, v);
+#else
+    const uint32_t l = left_or_zero(v);
+#endif
+#endif
+    const uint32_t L = __builtin_amdgcn_alignbit(v, l, 31);
+    const uint32_t R = __builtin_amdgcn_alignbit(r, v, 1);
     BitEnc::fa(L, v, R, s0, s1);
 }
 
@@ -779,8 +804,8 @@ struct Tunings {
     StepTuning t[2];  // [0] byte, [1] bit
     // temporal stencil: register rows per wave (window = kStackWaves * rows,
     // tile = window - 2K), per encoding [byte, bit]; fastest measured at
-    // 65536^2 with K = 32 (profiles/r01/tune_*_k32.jsonl)
-    int nr[2] = {48, 96};
+    // 65536^2 with K = 32 and hsum mode 2 (profiles/r01/tune_stacked_*_k32_hsum2.jsonl)
+    int nr[2] = {32, 48};
     Tunings() : t{{64, 2}, {16, 8}} {
         for (StepTuning &v : t) {
             if (const char *e = getenv("LIFE_STEP_ROWS")) v.rows = atoi(e);
@@ -801,7 +826,7 @@ StepTuning step_tuning(bool bit) { return tunings().t[bit ? 1 : 0]; }
 
 int temporal_rows(bool bit) {
     const int nr = tunings().nr[bit ? 1 : 0];
-    return temporal_rows_ok(nr) ? nr : (bit ? 96 : 48);
+    return temporal_rows_ok(nr) ? nr : (bit ? 48 : 32);
 }
 
 // Per register row and generation: bit_hsum = 2 DPP moves + 2 v_alignbit +

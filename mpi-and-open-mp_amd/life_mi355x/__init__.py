@@ -30,7 +30,8 @@ import numpy as np
 from .cfg import load_cfg, save_vtk, vtk_bytes  # noqa: F401
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liblife_mi355x.so")
+# LIFE_MI355X_LIB: load another build of the same library (experiments only)
+LIB_PATH = os.environ.get("LIFE_MI355X_LIB") or os.path.join(HERE, "liblife_mi355x.so")
 
 KERNEL_BYTE = 0
 KERNEL_BIT = 1
@@ -41,7 +42,7 @@ HALO_COLUMN, HALO_ROW = 0, 1
 OPT_SMALL_GRID, OPT_OVERLAP = 1, 2
 # LIFE_TEMPORAL_DEPTH(_BYTE): generations per halo exchange of the temporal layouts
 TEMPORAL_DEPTH = {"bit": 32, "byte": 32}
-TEMPORAL_ROWS = {"bit": 96, "byte": 48}  # default register rows per wave of the temporal tiles
+TEMPORAL_ROWS = {"bit": 48, "byte": 32}  # default register rows per wave of the temporal tiles
 
 # Every symbol include/life_mi355x.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = (
