@@ -91,7 +91,7 @@ int life_halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int k
  * `generations_per_exchange` is how many generations one halo exchange
  * feeds: 1 for the one-cell apron; for the temporally blocked stencil
  * (32-cell x-apron, K-row y-apron) K = LIFE_TEMPORAL_DEPTH (bit) or
- * LIFE_TEMPORAL_DEPTH_BYTE (byte), or 8/16/32 from the environment variables
+ * LIFE_TEMPORAL_DEPTH_BYTE (byte), or 16/24/32 from the environment variables
  * of the same names. */
 #define LIFE_TEMPORAL_DEPTH 32
 #define LIFE_TEMPORAL_DEPTH_BYTE 32
@@ -204,7 +204,7 @@ int life_dev_kernel_work(life_dev *d, double *cell_updates_per_launch, double *v
 int life_tune(int kernel, int rows, int depth);
 
 /* Temporal (generations_per_exchange = K > 1) tile height of encoding
- * `kernel` (-1: both): register rows per wave, 32/48/64/80/96; a tile is one
+ * `kernel` (-1: both): register rows per wave, 32/40/48/56/64/96; a tile is one
  * workgroup of 8 vertically stacked waves, 8*rows - 2K owned rows; 0 keeps
  * the current values (defaults bit 48, byte 32, by measurement);
  * LIFE_TEMPORAL_ROWS / LIFE_TEMPORAL_ROWS_BYTE override at load time. */

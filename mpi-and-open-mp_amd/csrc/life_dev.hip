@@ -884,7 +884,7 @@ int life_tune(int kernel, int rows, int depth) {
 }
 
 int life_tune_temporal(int kernel, int rows) {
-    if ((rows && rows != 32 && rows != 48 && rows != 64 && rows != 80 && rows != 96) || kernel < -1 ||
+    if ((rows && rows != 32 && rows != 40 && rows != 48 && rows != 56 && rows != 64 && rows != 96) || kernel < -1 ||
         kernel > LIFE_KERNEL_BIT)
         return LIFE_EINVAL;
     life::set_temporal_rows(kernel, rows);

@@ -63,7 +63,7 @@ constexpr int64_t kTemporalSlackRows = 8 * 96;
 // Up to 4 disjoint tile regions in one launch.
 hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, const TileRegion *r, int nreg,
                         int m, Wrap wrap, hipStream_t s);
-int temporal_rows(bool bit);      // register rows per wave (32/48/64/80/96)
+int temporal_rows(bool bit);      // register rows per wave (32/40/48/56/64/96)
 // VALU instructions the lanes at one lane position of a tile's waves issue
 // for m generations (the op-count model of life_kernels.hip tstep_kernel,
 // checked against the SQ_INSTS_VALU counter in profiles/); x 64 lanes x tiles.

@@ -819,7 +819,7 @@ Tunings &tunings() {
     static Tunings t;
     return t;
 }
-bool temporal_rows_ok(int nr) { return nr == 32 || nr == 48 || nr == 64 || nr == 80 || nr == 96; }
+bool temporal_rows_ok(int nr) { return nr == 32 || nr == 40 || nr == 48 || nr == 56 || nr == 64 || nr == 96; }
 }  // namespace
 
 StepTuning step_tuning(bool bit) { return tunings().t[bit ? 1 : 0]; }
@@ -924,10 +924,11 @@ template <bool BYTE, int K>
 hipError_t launch_k(const TArgs &a, Wrap wrap, unsigned grid, hipStream_t s) {
     switch (temporal_rows(!BYTE)) {
     case 32: return launch_t<BYTE, 32, K>(a, wrap, grid, s);
-    case 48: return launch_t<BYTE, 48, K>(a, wrap, grid, s);
-    case 80: return launch_t<BYTE, 80, K>(a, wrap, grid, s);
+    case 40: return launch_t<BYTE, 40, K>(a, wrap, grid, s);
+    case 56: return launch_t<BYTE, 56, K>(a, wrap, grid, s);
+    case 64: return launch_t<BYTE, 64, K>(a, wrap, grid, s);
     case 96: return launch_t<BYTE, 96, K>(a, wrap, grid, s);
-    default: return launch_t<BYTE, 64, K>(a, wrap, grid, s);
+    default: return launch_t<BYTE, 48, K>(a, wrap, grid, s);
     }
 }
 }  // namespace
@@ -944,7 +945,7 @@ TileGeom tile_geom(const life_layout &L) {
 hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, const TileRegion *r, int nreg,
                         int m, Wrap wrap, hipStream_t s) {
     const int K = L.generations_per_exchange;
-    if (nreg < 0 || nreg > kMaxRegions || m > K || (K != 8 && K != 16 && K != 32) || L.yapron != K)
+    if (nreg < 0 || nreg > kMaxRegions || m > K || (K != 16 && K != 24 && K != 32) || L.yapron != K)
         return hipErrorInvalidValue;
     TArgs a;
     a.in = in;
@@ -969,9 +970,9 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
     const unsigned grid = (unsigned)a.first[a.nreg];  // one workgroup per tile
     if (is_bit(L))
         return K == 16 ? launch_k<false, 16>(a, wrap, grid, s)
-                       : K == 32 ? launch_k<false, 32>(a, wrap, grid, s) : launch_k<false, 8>(a, wrap, grid, s);
+                       : K == 24 ? launch_k<false, 24>(a, wrap, grid, s) : launch_k<false, 32>(a, wrap, grid, s);
     return K == 16 ? launch_k<true, 16>(a, wrap, grid, s)
-                   : K == 32 ? launch_k<true, 32>(a, wrap, grid, s) : launch_k<true, 8>(a, wrap, grid, s);
+                   : K == 24 ? launch_k<true, 24>(a, wrap, grid, s) : launch_k<true, 32>(a, wrap, grid, s);
 }
 
 int64_t small_lds_bytes(const life_layout &L) {
