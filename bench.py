@@ -173,7 +173,7 @@ def main():
         gens_per_launch = updates_per_launch / (bytes_per_launch / (0.25 if a.kernel == "bit" else 2.0)) \
             if bytes_per_launch > 0 else 0.0
         temporal = life.layout().generations_per_exchange > 1
-        variant = a.kernel + ("_temporal" if temporal else ("_onegen" if a.kernel == "bit" else ""))
+        variant = a.kernel + ("_temporal" if temporal else "_onegen")
         traffic = load_traffic(variant, a.size) if a.workload == "weak" else None
         out = {
             "metric": "Gcell-updates/sec at 1/2/4/8 MI355X + % of HBM roofline, bit-exact",

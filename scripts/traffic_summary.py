@@ -8,10 +8,11 @@ MI355X_MICROARCH.md's HBM section prescribes for gfx950:
 * 16-B-per-lane streaming kernels (step_kernel, byte and one-generation
   bit): FETCH_SIZE reports half the bytes of wide coalesced reads, so it is
   doubled; WRITE_SIZE is exact for 16-B streaming stores.
-* the temporal bit kernel (tstep_kernel) loads and stores 4 B per lane:
-  an access width the guide lists as uncalibrated, so its entry carries the
-  raw counter values and `calibrated: false`, and bench.py reports its
-  `traffic` as null rather than an unverified absolute.
+* the temporal byte kernel moves 2 x 16 B per lane: calibrated as above;
+* the temporal bit kernel (tstep_kernel) loads and stores 4 B per lane, an
+  access width the guide lists as uncalibrated: scripts/calib_4b.hip copies
+  1 GiB with 4-B lanes and reads FETCH_SIZE = 0.500 GiB, WRITE_SIZE =
+  1.000 GiB (profiles/r01/calib_4b_*.csv), so the same x2 / x1 applies.
 
 Only full-length launches are summarised (the median over the dispatches of
 the dominant kernel).
@@ -29,8 +30,9 @@ d = os.path.join(ROOT, "profiles", rnd)
 
 VARIANTS = {  # variant -> (kernel-name substring, calibrated 16-B access)
     "bit_onegen": ("step_kernel<life::(anonymous namespace)::BitEnc", True),
-    "byte": ("step_kernel<life::(anonymous namespace)::ByteEnc", True),
-    "bit_temporal": ("tstep_kernel", False),
+    "byte_onegen": ("step_kernel<life::(anonymous namespace)::ByteEnc", True),
+    "bit_temporal": ("tstep_kernel<false", True),    # 4 B per lane (calib_4b)
+    "byte_temporal": ("tstep_kernel<true", True),    # 2 x 16 B per lane
 }
 
 out = {}
@@ -55,7 +57,8 @@ for var, (needle, calibrated) in VARIANTS.items():
         out[key] = round(fetch + vals["WRITE_SIZE"])
         out[key + "_detail"] = {"fetch_bytes_corrected": round(fetch), "fetch_size_raw_bytes": round(vals["FETCH_SIZE"]),
                                 "write_bytes": round(vals["WRITE_SIZE"]), "source": f"profiles/{rnd}/pmc_*_{var}.csv",
-                                "correction": "FETCH_SIZE x2 (gfx950, 16 B/lane streaming reads)", "calibrated": True}
+                                "correction": "FETCH_SIZE x2 (gfx950; 16 B/lane per MI355X_MICROARCH.md, 4 B/lane "
+                                              "by scripts/calib_4b.hip)", "calibrated": True}
     else:
         out[key] = None
         out[key + "_detail"] = {"fetch_size_raw_bytes": round(vals["FETCH_SIZE"]),
