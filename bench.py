@@ -208,9 +208,9 @@ def main():
             tops = valu_per_launch / (avg_ms * 1e-3) / 1e12
             out["valu"] = {"bound": "valu", "achieved": round(tops, 2), "peak": round(VALU_PEAK_TOPS, 2),
                            "unit": "Tlane-op/s", "frac": round(tops / VALU_PEAK_TOPS, 4),
-                           "ops_per_launch": valu_per_launch, "model": "14 VALU ops per register row "
-                           "and generation (life_kernels.hip tstep_valu_per_tile_lane), within 3% of "
-                           "SQ_INSTS_VALU (profiles/r01/pmc_SQ_bit_temporal.csv)"}
+                           "ops_per_launch": valu_per_launch, "model": "13 VALU ops per register row "
+                           "and generation + byte pack/unpack (life_kernels.hip tstep_valu_per_tile_lane), "
+                           "within 2% of SQ_INSTS_VALU (profiles/r01/pmc_SQ_*_temporal.csv)"}
         if n_gpus == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
         print(json.dumps(out), flush=True)

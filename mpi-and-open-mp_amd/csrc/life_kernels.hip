@@ -829,12 +829,14 @@ int temporal_rows(bool bit) {
     return temporal_rows_ok(nr) ? nr : (bit ? 48 : 32);
 }
 
-// Per register row and generation: bit_hsum = 2 DPP moves + 2 v_alignbit +
+// Per register row and generation: bit_hsum = 2 neighbour fetches (DPP on
+// the VALU or ds_bpermute on the LDS pipe, LIFE_HSUM_MODE) + 2 v_alignbit +
 // 2 v_bitop3, rule1 = 8 v_bitop3; kStackWaves waves of temporal_rows() rows
 // per tile; the byte encoding adds pack (8 v_dot4 + 3 shifts) and unpack
 // (8 x bfe/mul24/and) once per row and launch.
+constexpr double kValuPerRow = LIFE_HSUM_MODE == 0 ? 14.0 : LIFE_HSUM_MODE == 1 ? 12.0 : 13.0;
 double tstep_valu_per_tile_lane(int m, bool byte) {
-    return (double)kStackWaves * (double)temporal_rows(!byte) * (14.0 * (double)m + (byte ? 35.0 : 0.0));
+    return (double)kStackWaves * (double)temporal_rows(!byte) * (kValuPerRow * (double)m + (byte ? 35.0 : 0.0));
 }
 
 void set_temporal_rows(int kernel, int nr) {
