@@ -328,9 +328,12 @@ struct TArgs {
     int64_t pitch, xoff, W, h, ya;  // W = 32-bit words per owned row
     // up to kMaxRegions tile regions in one launch (the boundary ring of a
     // partitioned shard); workgroup b belongs to the region with first[k] <= b
-    int64_t tx0[kMaxRegions], tx1[kMaxRegions], ty0[kMaxRegions], first[kMaxRegions + 1];
+    int64_t tx0[kMaxRegions], tx1[kMaxRegions], ty0[kMaxRegions], ty1[kMaxRegions], first[kMaxRegions + 1];
     int32_t nreg, m;
 };
+#ifndef LIFE_XCD_ORDER
+#define LIFE_XCD_ORDER 0
+#endif
 
 // Neighbour words with bound_ctrl: lanes 0 / 63 read 0 (their outer bits are
 // allowed to be wrong), and the DPP move needs no `old` operand copy.
@@ -393,12 +396,29 @@ __global__ __launch_bounds__(64 * kStackWaves, 4) void tstep_kernel(TArgs a) {  
     const int lane = threadIdx.x & 63;
     // wave index: uniform, so every row address below is scalar (SALU) math
     const int wi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t nwg = a.first[a.nreg];
+    if ((int64_t)blockIdx.x >= nwg) return;  // whole workgroup
+#if LIFE_XCD_ORDER
+    // XCD-aware order (build-time switch, off: bit unchanged, byte -11 %,
+    // profiles/r01/xcd_order.txt): the dispatcher deals workgroups round-robin over the 8
+    // XCDs; give each XCD a contiguous run of tiles, walked down tile columns,
+    // so the 2K ghost rows a tile shares with the one below it are re-read
+    // from that XCD's L2 (bijective for any nwg).
+    const int64_t b = blockIdx.x, x = b % 8, per = nwg / 8, rem = nwg % 8;
+    const int64_t wg = (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + b / 8;
+#else
     const int64_t wg = blockIdx.x;
-    if (wg >= a.first[a.nreg]) return;  // whole workgroup
+#endif
     int k = 0;
     while (k + 1 < a.nreg && wg >= a.first[k + 1]) ++k;
-    const int64_t ntx = a.tx1[k] - a.tx0[k], wr = wg - a.first[k];
+    const int64_t wr = wg - a.first[k];
+#if LIFE_XCD_ORDER
+    const int64_t nty = a.ty1[k] - a.ty0[k];
+    const int64_t ty = a.ty0[k] + wr % nty, tx = a.tx0[k] + wr / nty;
+#else
+    const int64_t ntx = a.tx1[k] - a.tx0[k];
     const int64_t tx = a.tx0[k] + wr % ntx, ty = a.ty0[k] + wr / ntx;
+#endif
     const int64_t j = tx * 62 + lane - 1;  // word column of this lane
     int64_t jl;
     if (WRAPX) {
@@ -966,6 +986,7 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
         a.tx0[n] = r[k].tx0;
         a.tx1[n] = r[k].tx1;
         a.ty0[n] = r[k].ty0;
+        a.ty1[n] = r[k].ty1;
         a.first[n + 1] = a.first[n] + (r[k].tx1 - r[k].tx0) * (r[k].ty1 - r[k].ty0);
     }
     if (a.nreg == 0 || m <= 0) return hipSuccess;

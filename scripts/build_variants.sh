@@ -19,6 +19,7 @@ for v in "$@"; do
         hsum2) build hsum2 -DLIFE_HSUM_MODE=2 ;;
         nw16) build nw16 -DLIFE_STACK_WAVES=16 ;;
         nw4) build nw4 -DLIFE_STACK_WAVES=4 ;;
+        xcd) build xcd -DLIFE_XCD_ORDER=1 ;;
         *) echo "unknown variant $v"; exit 1 ;;
     esac
 done
