@@ -159,6 +159,12 @@ int life_dev_step(life_dev *d, int64_t generations);
  * In rank mode only the root writes `grid` (others may pass NULL). Blocking. */
 int life_dev_gather(life_dev *d, uint8_t *grid);
 
+/* The same collect, formatted on the device as the cell-data body of
+ * life_save_vtk (life_cart.c:181-185): "%d\n" per cell, y outer, x inner --
+ * 2*nx*ny bytes of '0'/'1' and '\n' written to `body` (root only in rank
+ * mode).  The caller writes the 10 header lines in front (driver/life.c). */
+int life_dev_gather_vtk(life_dev *d, char *body);
+
 /* Live cells over the whole grid (all ranks). Blocking. */
 int64_t life_dev_live_count(life_dev *d);
 

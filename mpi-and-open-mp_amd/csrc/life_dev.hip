@@ -81,6 +81,8 @@ struct Shard {
     unsigned long long *d_count = nullptr;  // census: live count, checksum
     unsigned long long *h_count = nullptr;  // pinned, 2 entries
     uint8_t *sink = nullptr;  // stencil stores of lanes outside a region
+    uint8_t *stage = nullptr;  // gather staging (grows on demand)
+    size_t stage_bytes = 0;
     std::vector<life_halo_op> plan;
     std::vector<TimedLaunch> timers;
     size_t timers_used = 0;
@@ -150,7 +152,7 @@ void shard_free(Shard &s) {
         if (t.a) (void)hipEventDestroy(t.a);
         if (t.b) (void)hipEventDestroy(t.b);
     }
-    for (uint8_t *p : {s.buf[0], s.buf[1], s.col_send, s.col_recv, s.sink})
+    for (uint8_t *p : {s.buf[0], s.buf[1], s.col_send, s.col_recv, s.sink, s.stage})
         if (p) (void)hipFree(p);
     if (s.d_count) (void)hipFree(s.d_count);
     if (s.h_count) (void)hipHostFree(s.h_count);
@@ -727,62 +729,101 @@ int life_dev_sync(life_dev *d) {
     return LIFE_OK;
 }
 
-int life_dev_gather(life_dev *d, uint8_t *grid) {
-    if (!d) return LIFE_EINVAL;
+}  // extern "C"
+
+namespace {
+// Device staging of one shard's export, kept between calls (a 65536^2 grid's
+// frame is 4 GiB dense / 8 GiB as VTK text: no allocation per frame).
+int stage_buffer(Shard &s, size_t bytes, uint8_t **out) {
+    if (s.stage_bytes < bytes) {
+        if (s.stage) HIPCHK(hipFree(s.stage));
+        s.stage = nullptr;
+        s.stage_bytes = 0;
+        HIPCHK(hipMalloc(&s.stage, bytes));
+        s.stage_bytes = bytes;
+    }
+    *out = s.stage;
+    return LIFE_OK;
+}
+
+// life_collect for `bpc` output bytes per cell: 1 = dense 0/1 cells
+// (export kernel), 2 = the VTK "%d\n" cell text (vtk kernel).  Every shard
+// exports its block on the device; in-process shards copy straight into
+// place, rank mode sends the blocks to the root (world-1) over RCCL.
+int gather_impl(life_dev *d, uint8_t *out, int bpc) {
     const int root = d->world - 1;  // life_collect: cart rank of (dims0-1, dims1-1)
     const bool have_root = find_local(d, root) != nullptr;
-    if (have_root && !grid) return LIFE_EINVAL;
+    if (have_root && !out) return LIFE_EINVAL;
     CHK(life_dev_sync(d));
+    auto export_block = [&](Shard &s, uint8_t **stage) -> int {
+        const life_layout &L = s.lay;
+        CHK(stage_buffer(s, (size_t)(L.w * L.h * bpc), stage));
+        if (bpc == 1)
+            HIPCHK(life::launch_export_block(L, s.buf[s.cur], *stage, s.stream));
+        else
+            HIPCHK(life::launch_vtk_block(L, s.buf[s.cur], *stage, s.stream));
+        return LIFE_OK;
+    };
+    auto place = [&](const life_layout &L, const uint8_t *src) -> int {
+        // blocking: `out` is the caller's pageable memory
+        HIPCHK(hipMemcpy2D(out + (L.y0 * d->nx + L.x0) * bpc, (size_t)(d->nx * bpc), src, (size_t)(L.w * bpc),
+                           (size_t)(L.w * bpc), (size_t)L.h, hipMemcpyDeviceToHost));
+        return LIFE_OK;
+    };
     if (!d->rank_mode) {
-        // Every shard is in this process: each exports its block and copies it
-        // into place (parallel D2H over each device's own link).
         for (Shard &s : d->shards) {
-            const life_layout &L = s.lay;
             HIPCHK(hipSetDevice(s.device));
-            uint8_t *stage = nullptr;
-            HIPCHK(hipMalloc(&stage, (size_t)(L.w * L.h)));
-            HIPCHK(life::launch_export_block(L, s.buf[s.cur], stage, s.stream));
+            uint8_t *stage;
+            CHK(export_block(s, &stage));
+        }
+        for (Shard &s : d->shards) {  // every export is queued before the first copy waits
+            HIPCHK(hipSetDevice(s.device));
             HIPCHK(hipStreamSynchronize(s.stream));
-            HIPCHK(hipMemcpy2D(grid + L.y0 * d->nx + L.x0, (size_t)d->nx, stage, (size_t)L.w, (size_t)L.w,
-                               (size_t)L.h, hipMemcpyDeviceToHost));  // blocking: pageable destination
-            HIPCHK(hipFree(stage));
+            CHK(place(s.lay, s.stage));
         }
         return LIFE_OK;
     }
-    // Rank mode: device-side gather to the root over RCCL, then D2H at the root.
     Shard &s = d->shards[0];
     HIPCHK(hipSetDevice(s.device));
+    uint8_t *stage;
+    CHK(export_block(s, &stage));
+    if (s.rank != root) {
+        NCCLCHK(ncclSend(stage, (size_t)(s.lay.w * s.lay.h * bpc), ncclUint8, root, s.comm, s.stream));
+        HIPCHK(hipStreamSynchronize(s.stream));
+        return LIFE_OK;
+    }
+    HIPCHK(hipStreamSynchronize(s.stream));
+    CHK(place(s.lay, stage));
     int64_t maxb = 0;
     for (int r = 0; r < d->world; r++) {
         life_layout L;
         CHK(life_layout_query(d->nx, d->ny, d->dims[0], d->dims[1], r, d->kernel, &L));
         if (L.w * L.h > maxb) maxb = L.w * L.h;
     }
-    uint8_t *stage = nullptr, *rstage = nullptr;
-    HIPCHK(hipMalloc(&stage, (size_t)(s.lay.w * s.lay.h)));
-    HIPCHK(life::launch_export_block(s.lay, s.buf[s.cur], stage, s.stream));
-    int rc = LIFE_OK;
-    if (s.rank != root) {
-        NCCLCHK(ncclSend(stage, (size_t)(s.lay.w * s.lay.h), ncclUint8, root, s.comm, s.stream));
-    } else {
+    // the root's own block is placed: its staging now receives the others'
+    CHK(stage_buffer(s, (size_t)(maxb * bpc), &stage));
+    for (int r = 0; r < d->world; r++) {
+        if (r == root) continue;
+        life_layout L;
+        CHK(life_layout_query(d->nx, d->ny, d->dims[0], d->dims[1], r, d->kernel, &L));
+        NCCLCHK(ncclRecv(stage, (size_t)(L.w * L.h * bpc), ncclUint8, r, s.comm, s.stream));
         HIPCHK(hipStreamSynchronize(s.stream));
-        HIPCHK(hipMemcpy2D(grid + s.lay.y0 * d->nx + s.lay.x0, (size_t)d->nx, stage, (size_t)s.lay.w,
-                           (size_t)s.lay.w, (size_t)s.lay.h, hipMemcpyDeviceToHost));
-        HIPCHK(hipMalloc(&rstage, (size_t)maxb));
-        for (int r = 0; r < d->world && rc == LIFE_OK; r++) {
-            if (r == root) continue;
-            life_layout L;
-            CHK(life_layout_query(d->nx, d->ny, d->dims[0], d->dims[1], r, d->kernel, &L));
-            NCCLCHK(ncclRecv(rstage, (size_t)(L.w * L.h), ncclUint8, r, s.comm, s.stream));
-            HIPCHK(hipStreamSynchronize(s.stream));
-            HIPCHK(hipMemcpy2D(grid + L.y0 * d->nx + L.x0, (size_t)d->nx, rstage, (size_t)L.w, (size_t)L.w,
-                               (size_t)L.h, hipMemcpyDeviceToHost));
-        }
+        CHK(place(L, stage));
     }
-    HIPCHK(hipStreamSynchronize(s.stream));
-    HIPCHK(hipFree(stage));
-    if (rstage) HIPCHK(hipFree(rstage));
-    return rc;
+    return LIFE_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int life_dev_gather(life_dev *d, uint8_t *grid) {
+    if (!d) return LIFE_EINVAL;
+    return gather_impl(d, grid, 1);
+}
+
+int life_dev_gather_vtk(life_dev *d, char *body) {
+    if (!d) return LIFE_EINVAL;
+    return gather_impl(d, reinterpret_cast<uint8_t *>(body), 2);
 }
 
 static int census(life_dev *d, unsigned long long out[2]) {

@@ -96,6 +96,9 @@ hipError_t launch_import_block(const life_layout &L, const uint8_t *dense, uint8
 hipError_t launch_export_block(const life_layout &L, const uint8_t *buf, uint8_t *dense,
                                hipStream_t s);
 
+// The block's VTK cell data: '0'/'1' + '\n' per owned cell, rows of 2w bytes.
+hipError_t launch_vtk_block(const life_layout &L, const uint8_t *buf, uint8_t *out, hipStream_t s);
+
 // Counter-based synthetic init of the owned cells (global indices).
 hipError_t launch_fill_random(const life_layout &L, int64_t nx, uint64_t key, uint32_t thr32,
                               uint8_t *buf, hipStream_t s);

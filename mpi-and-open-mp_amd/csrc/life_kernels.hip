@@ -730,6 +730,44 @@ __global__ void export_kernel(const uint8_t *buf, uint8_t *dense, int64_t pitch,
     }
 }
 
+// VTK CELL_DATA body of a block (life_save_vtk, life_cart.c:181-185: "%d\n"
+// per cell, x fastest): 2 bytes per cell, '0'/'1' then '\n', row pitch 2w.
+// One thread per 8 cells of a row (16 output bytes); 2-D grid, y strides rows.
+__device__ __forceinline__ uint64_t vtk4(uint32_t cells4) {  // 4 cells, bit k -> ASCII pair k
+    uint64_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v |= (uint64_t)(0x0A30u | ((cells4 >> k) & 1u)) << (16 * k);
+    return v;
+}
+template <bool BIT>
+__global__ void vtk_kernel(const uint8_t *buf, int64_t pitch, int64_t ya, int64_t xoff, int64_t w, int64_t h,
+                           uint8_t *out) {
+    const int64_t x0 = 8 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+    if (x0 >= w) return;
+    const int n = w - x0 < 8 ? (int)(w - x0) : 8;
+    const bool vec = (w & 7) == 0;  // 16-B aligned output rows
+    for (int64_t y = blockIdx.y; y < h; y += gridDim.y) {
+        const uint8_t *row = buf + (y + ya) * pitch + xoff;
+        uint32_t c;  // cell k at bit k
+        if (BIT) {
+            c = row[x0 >> 3];  // x0 is a multiple of 8: one byte of the little-endian words
+        } else {
+            c = 0;
+            for (int k = 0; k < n; ++k) c |= (uint32_t)(row[x0 + k] & 1u) << k;
+        }
+        uint8_t *o = out + y * 2 * w + 2 * x0;
+        if (vec && n == 8) {
+            *reinterpret_cast<uint4 *>(o) = make_uint4((uint32_t)vtk4(c), (uint32_t)(vtk4(c) >> 32),
+                                                       (uint32_t)vtk4(c >> 4), (uint32_t)(vtk4(c >> 4) >> 32));
+        } else {
+            for (int k = 0; k < n; ++k) {
+                o[2 * k] = (uint8_t)('0' + ((c >> k) & 1u));
+                o[2 * k + 1] = '\n';
+            }
+        }
+    }
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
     z += 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -1067,6 +1105,15 @@ hipError_t launch_fill_random(const life_layout &L, int64_t nx, uint64_t key, ui
     else
         fill_random_kernel<16><<<g, 256, 0, s>>>(buf, L.pitch, L.yapron, L.xoff, L.w, L.h, L.units, L.x0, L.y0, nx,
                                                  key, thr32);
+    return hipGetLastError();
+}
+
+hipError_t launch_vtk_block(const life_layout &L, const uint8_t *buf, uint8_t *out, hipStream_t s) {
+    const dim3 grid(blocks_for((L.w + 7) / 8, 256), (unsigned)(L.h < 8192 ? L.h : 8192));
+    if (is_bit(L))
+        vtk_kernel<true><<<grid, 256, 0, s>>>(buf, L.pitch, L.yapron, L.xoff, L.w, L.h, out);
+    else
+        vtk_kernel<false><<<grid, 256, 0, s>>>(buf, L.pitch, L.yapron, L.xoff, L.w, L.h, out);
     return hipGetLastError();
 }
 

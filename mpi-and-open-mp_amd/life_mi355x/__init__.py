@@ -27,7 +27,7 @@ import os
 
 import numpy as np
 
-from .cfg import load_cfg, save_vtk, vtk_bytes  # noqa: F401
+from .cfg import bits_bytes, load_bits, load_cfg, save_vtk, vtk_bytes, vtk_header  # noqa: F401
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 # LIFE_MI355X_LIB: load another build of the same library (experiments only)
@@ -52,7 +52,7 @@ ABI_SYMBOLS = (
     "life_dev_step", "life_dev_gather", "life_dev_live_count", "life_dev_sync",
     "life_dev_layout", "life_dev_world", "life_dev_set_timing", "life_dev_kernel_stats",
     "life_tune", "life_tune_temporal", "life_dev_configure", "life_dev_kernel_work", "life_dev_checksum",
-    "life_dev_destroy",
+    "life_dev_gather_vtk", "life_dev_destroy",
 )
 
 
@@ -110,6 +110,7 @@ def _lib():
         L.life_dev_fill_random.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint32]
         L.life_dev_step.argtypes = [vp, i64]
         L.life_dev_gather.argtypes = [vp, P(ctypes.c_uint8)]
+        L.life_dev_gather_vtk.argtypes = [vp, ctypes.c_char_p]
         L.life_dev_live_count.argtypes = [vp]
         L.life_dev_live_count.restype = i64
         L.life_dev_sync.argtypes = [vp]
@@ -244,6 +245,13 @@ class Life:
             out = np.empty((self.ny, self.nx), dtype=np.uint8)
         _check(_lib().life_dev_gather(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))), "gather")
         return out
+
+    def gather_vtk(self) -> bytes:
+        """life_dev_gather_vtk: the whole VTK file of the current grid, with
+        the cell text formatted on the device (== save_vtk of gather())."""
+        body = ctypes.create_string_buffer(2 * self.nx * self.ny)
+        _check(_lib().life_dev_gather_vtk(self._h, body), "gather_vtk")
+        return vtk_header(self.nx, self.ny) + body.raw
 
     def live_count(self) -> int:
         return _check(_lib().life_dev_live_count(self._h), "live_count")

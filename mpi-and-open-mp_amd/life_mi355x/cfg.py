@@ -56,6 +56,29 @@ def vtk_bytes(grid: np.ndarray) -> bytes:
     return vtk_header(nx, ny) + body.tobytes()
 
 
+def bits_bytes(grid: np.ndarray, generation: int = 0) -> bytes:
+    """The driver's packed frame (--format bits): 'LIFEBITS 1 nx ny gen\\n'
+    then rows of ceil(nx/8) bytes, cell x at bit x&7 of byte x>>3."""
+    ny, nx = grid.shape
+    rows = np.packbits(grid.astype(bool), axis=1, bitorder="little")
+    return f"LIFEBITS 1 {nx} {ny} {generation}\n".encode() + rows.tobytes()
+
+
+def load_bits(path: str):
+    """-> (generation, grid[ny, nx] uint8) of a --format bits frame."""
+    with open(path, "rb") as f:
+        head = f.readline().split()
+        if len(head) != 5 or head[0] != b"LIFEBITS" or head[1] != b"1":
+            raise ValueError(f"{path}: not a LIFEBITS v1 frame")
+        nx, ny, gen = int(head[2]), int(head[3]), int(head[4])
+        raw = np.frombuffer(f.read(), dtype=np.uint8)
+    rb = (nx + 7) // 8
+    if raw.size != rb * ny:
+        raise ValueError(f"{path}: truncated")
+    grid = np.unpackbits(raw.reshape(ny, rb), axis=1, bitorder="little")[:, :nx]
+    return gen, np.ascontiguousarray(grid, dtype=np.uint8)
+
+
 def save_vtk(path: str, grid: np.ndarray) -> None:
     """life_save_vtk: creates ./vtk if missing (life_cart.c:163-166)."""
     if os.path.basename(os.path.dirname(path)) == "vtk" and not os.path.isdir(os.path.dirname(path)):

@@ -93,3 +93,34 @@ def test_driver_p46gun_big(gpu, tmp_path):
     assert r.returncode == 0, r.stderr
     assert md5((tmp_path / "vtk" / "life_000000.vtk").read_bytes()) == G["p46gun_big"]["frame0_md5"]
     assert md5((tmp_path / "vtk" / "life_010000.vtk").read_bytes()) == G["p46gun_big"]["gen10000_md5"]
+
+
+def test_driver_bits_frames_and_resume(gpu, tmp_path):
+    """--format bits writes packed frames equal to the reference's frames;
+    --resume from generation 40 continues the reference's frame sequence."""
+    frames = G["patterns"]["glider_10x10"]["frames"]
+    r = subprocess.run([DRIVER, os.path.join(GOLDEN, "cfg", "glider_10x10.cfg"), "--format", "bits"], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    for i in (0, 1, 39, 40, 99):
+        gen, g = gpu.load_bits(str(tmp_path / "vtk" / f"life_{i:06d}.bits"))
+        assert gen == i and md5(gpu.vtk_bytes(g)) == frames[str(i)][0], i
+    run2 = tmp_path / "resumed"
+    run2.mkdir()
+    r = subprocess.run([DRIVER, "--resume", str(tmp_path / "vtk" / "life_000040.bits"), "--steps", "60",
+                        "--save-steps", "10"], cwd=run2, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    for i in range(0, 60, 10):
+        assert md5((run2 / "vtk" / f"life_{i:06d}.vtk").read_bytes()) == frames[str(40 + i)][0], i
+
+
+@pytest.mark.parametrize("kernel", ["byte", "bit"])
+@pytest.mark.parametrize("nx,ny,shards", [(10, 10, 1), (37, 11, 1), (257, 131, 4), (1024, 300, 8), (5, 3, 1)])
+def test_gather_vtk_equals_host_format(gpu, oracle, kernel, nx, ny, shards):
+    """Device-formatted VTK text (life_dev_gather_vtk) == life_save_vtk of the
+    gathered cells, for widths that are and are not multiples of 8."""
+    g0 = oracle.fill_random(nx, ny, seed=nx * ny, density=0.5)
+    with gpu.Life(nx, ny, shards=shards, kernel=kernel, transport=gpu.XPORT_LOCAL) as life:
+        life.upload(g0)
+        life.step(3)
+        assert life.gather_vtk() == gpu.vtk_bytes(life.gather())

@@ -152,3 +152,13 @@ def test_temporal_mode_selection(lm, nx, ny, dims, temporal):
         assert (B.xapron, B.yapron, B.generations_per_exchange) == ((32, KB, KB) if tb else (1, 1, 1))
         if tb:  # room for the 32-byte right apron
             assert B.pitch >= B.xoff + B.w + 32
+
+
+def test_bits_frame_roundtrip(lm, oracle, tmp_path):
+    g = oracle.fill_random(37, 11, 4, 0.5)
+    p = tmp_path / "f.bits"
+    p.write_bytes(lm.bits_bytes(g, 123))
+    gen, back = lm.load_bits(str(p))
+    assert gen == 123
+    np.testing.assert_array_equal(back, g)
+    assert p.read_bytes().startswith(b"LIFEBITS 1 37 11 123\n") and len(p.read_bytes()) == 21 + 5 * 11
