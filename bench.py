@@ -49,9 +49,9 @@ VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    # defaults: whole multiples of the temporal kernel's 16 generations per launch
+    # defaults: whole multiples of the temporal kernel's 32 generations per launch
     p.add_argument("--steps", type=int, default=160)
-    p.add_argument("--warmup", type=int, default=16)
+    p.add_argument("--warmup", type=int, default=32)
     p.add_argument("--kernel", default="bit", choices=["bit", "byte"])
     p.add_argument("--size", type=int, default=65536, help="per-GPU block edge (weak scaling)")
     p.add_argument("--workload", default="weak", choices=["weak", "p46gun_big"])

@@ -31,12 +31,16 @@
  * defined for i >= -nx), and sizes are 64-bit.
  */
 #include <errno.h>
+#include <fcntl.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <time.h>
+#include <unistd.h>
 
 #include "life_mi355x.h"
 
@@ -56,46 +60,133 @@ static int64_t wrapi(int64_t i, int64_t n) { return ((i % n) + n) % n; }
 
 typedef struct {
     int64_t steps, save_steps, nx, ny;
-    int64_t ncells;   /* live-cell lines */
-    int64_t *cells;   /* x0 y0 x1 y1 ... */
+    uint8_t *grid; /* nx*ny 0/1 cells, row-major (NULL until loaded) */
 } cfg_t;
 
 /* .cfg loader: life_cart.c:92-111.  "steps\n save_steps\n nx ny\n" then one
- * "i j" live cell per line until EOF. */
-static int load_cfg(const char *path, cfg_t *c) {
-    FILE *f = fopen(path, "r");
-    if (!f) return LIFE_EIO;
-    long long v[4];
-    for (int k = 0; k < 4; k++)
-        if (fscanf(f, "%lld", &v[k]) != 1) {
-            fclose(f);
-            return LIFE_EIO;
-        }
-    c->steps = v[0];
-    c->save_steps = v[1];
-    c->nx = v[2];
-    c->ny = v[3];
-    int64_t cap = 1024;
-    c->cells = (int64_t *)malloc(sizeof(int64_t) * 2 * cap);
-    c->ncells = 0;
-    for (;;) {
-        long long i, j;
-        int r = fscanf(f, "%lld", &i);
-        if (r == EOF) break;
-        if (r != 1 || fscanf(f, "%lld", &j) != 1) {
-            fclose(f);
-            return LIFE_EIO;
-        }
-        if (c->ncells == cap) {
-            cap *= 2;
-            c->cells = (int64_t *)realloc(c->cells, sizeof(int64_t) * 2 * cap);
-        }
-        c->cells[2 * c->ncells] = i;
-        c->cells[2 * c->ncells + 1] = j;
-        c->ncells++;
+ * "i j" live cell per line until EOF; cell (i, j) wraps periodically
+ * (life_cart.c:106-109).  The file is mapped and the cell lines are parsed by
+ * up to 16 threads, each on a line-aligned chunk writing straight into the
+ * grid (a 32768^2 random pattern is a ~6 GB file).  A chunk whose token count
+ * is odd (pairs not one per line) sends the whole body to the sequential
+ * parser, which pairs tokens across lines like the reference's fscanf loop. */
+typedef struct {
+    const char *p, *end;
+    int64_t nx, ny;
+    uint8_t *grid;
+    int status; /* 0 ok, 1 odd token count, 2 malformed */
+} parse_job;
+
+static int next_int(const char **pp, const char *end, long long *v) {
+    const char *p = *pp;
+    while (p < end && (*p == ' ' || *p == '\n' || *p == '\t' || *p == '\r')) p++;
+    if (p == end) {
+        *pp = p;
+        return 0; /* EOF */
     }
-    fclose(f);
-    return LIFE_OK;
+    int neg = 0;
+    if (*p == '-' || *p == '+') neg = *p++ == '-';
+    if (p == end || *p < '0' || *p > '9') return -1;
+    long long x = 0;
+    while (p < end && *p >= '0' && *p <= '9') x = x * 10 + (*p++ - '0');
+    if (p < end && !(*p == ' ' || *p == '\n' || *p == '\t' || *p == '\r')) return -1;
+    *v = neg ? -x : x;
+    *pp = p;
+    return 1;
+}
+
+static void *parse_cells(void *arg) {
+    parse_job *jb = (parse_job *)arg;
+    const char *p = jb->p;
+    long long i, j;
+    for (;;) {
+        int r = next_int(&p, jb->end, &i);
+        if (r == 0) break;
+        if (r < 0) {
+            jb->status = 2;
+            return NULL;
+        }
+        r = next_int(&p, jb->end, &j);
+        if (r == 0) {
+            jb->status = 1;
+            return NULL;
+        }
+        if (r < 0) {
+            jb->status = 2;
+            return NULL;
+        }
+        jb->grid[wrapi(j, jb->ny) * jb->nx + wrapi(i, jb->nx)] = 1; /* u0[ind(i, j)] = 1 */
+    }
+    jb->status = 0;
+    return NULL;
+}
+
+static int load_cfg(const char *path, cfg_t *c, int64_t o_nx, int64_t o_ny) {
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) return LIFE_EIO;
+    struct stat st;
+    if (fstat(fd, &st) != 0) {
+        close(fd);
+        return LIFE_EIO;
+    }
+    const size_t len = (size_t)st.st_size;
+    const char *base = len ? (const char *)mmap(NULL, len, PROT_READ, MAP_PRIVATE, fd, 0) : "";
+    close(fd);
+    if (base == MAP_FAILED) return LIFE_EIO;
+    const char *p = base, *end = base + len;
+    long long v[4];
+    int rc = LIFE_OK;
+    for (int k = 0; k < 4 && rc == LIFE_OK; k++)
+        if (next_int(&p, end, &v[k]) != 1) rc = LIFE_EIO;
+    if (rc == LIFE_OK && (v[2] <= 0 || v[3] <= 0)) rc = LIFE_EIO;
+    if (rc == LIFE_OK) {
+        c->steps = v[0];
+        c->save_steps = v[1];
+        c->nx = o_nx > 0 ? o_nx : v[2]; /* --nx/--ny override the header before the cells wrap */
+        c->ny = o_ny > 0 ? o_ny : v[3];
+        c->grid = (uint8_t *)calloc((size_t)(c->nx * c->ny), 1);
+        if (!c->grid) rc = LIFE_ENOMEM;
+    }
+    if (rc == LIFE_OK) {
+        enum { kMaxThreads = 16 };
+        long np = sysconf(_SC_NPROCESSORS_ONLN);
+        int nt = (int)((size_t)(end - p) / (1 << 22)); /* >= 4 MiB per thread */
+        if (nt > kMaxThreads) nt = kMaxThreads;
+        if (nt > np) nt = (int)np;
+        if (nt < 1) nt = 1;
+        parse_job jobs[kMaxThreads];
+        pthread_t th[kMaxThreads];
+        const char *q = p;
+        for (int t = 0; t < nt; t++) { /* line-aligned chunks */
+            const char *e = t == nt - 1 ? end : p + (size_t)(end - p) * (size_t)(t + 1) / (size_t)nt;
+            while (e < end && *e != '\n') e++;
+            jobs[t] = (parse_job){q, e, c->nx, c->ny, c->grid, 0};
+            q = e;
+        }
+        int started = 0;
+        for (int t = 1; t < nt; t++)
+            if (pthread_create(&th[t], NULL, parse_cells, &jobs[t]) == 0) started = t;
+            else break;
+        parse_cells(&jobs[0]);
+        for (int t = 1; t <= started; t++) pthread_join(th[t], NULL);
+        for (int t = started + 1; t < nt; t++) parse_cells(&jobs[t]); /* threads that did not start */
+        int odd = 0;
+        for (int t = 0; t < nt; t++) {
+            if (jobs[t].status == 2) rc = LIFE_EIO;
+            odd |= jobs[t].status == 1;
+        }
+        if (rc == LIFE_OK && odd) { /* pairs split across lines: one sequential pass */
+            parse_job all = {p, end, c->nx, c->ny, c->grid, 0};
+            parse_cells(&all);
+            if (all.status) rc = LIFE_EIO;
+        }
+    }
+    if (len) munmap((void *)base, len);
+    if (rc != LIFE_OK) {
+        free(c->grid);
+        c->grid = NULL;
+    }
+    return rc;
 }
 
 static FILE *open_frame(const char *path) {
@@ -216,8 +307,8 @@ int main(int argc, char **argv) {
         return 1;
     }
 
-    cfg_t c = {0, 1, 0, 0, 0, NULL};
-    if (cfg_path && load_cfg(cfg_path, &c) != LIFE_OK) {
+    cfg_t c = {0, 1, 0, 0, NULL};
+    if (cfg_path && load_cfg(cfg_path, &c, resume ? -1 : o_nx, resume ? -1 : o_ny) != LIFE_OK) {
         fprintf(stderr, "life_mi355x: cannot read config '%s'\n", cfg_path);
         return 1;
     }
@@ -239,9 +330,9 @@ int main(int argc, char **argv) {
     life_dev *d = NULL;
     int rc = life_dev_create(c.nx, c.ny, gpus, kernel, &d);
     if (rc) die("create", rc);
-    uint8_t *grid = NULL; /* dense cells: .cfg loading and bits frames */
+    uint8_t *grid = NULL; /* dense cells: bits frames */
     char *body = NULL;    /* VTK cell text */
-    if ((vtk && bits) || (!have_random && !resume)) {
+    if (vtk && bits) {
         grid = (uint8_t *)calloc((size_t)(c.nx * c.ny), 1);
         if (!grid) die("host grid", LIFE_ENOMEM);
     }
@@ -255,12 +346,11 @@ int main(int argc, char **argv) {
     } else if (have_random) {
         rc = life_dev_fill_random(d, seed, density >= 1.0 ? 0xFFFFFFFFu : (uint32_t)(density * 4294967296.0));
     } else {
-        for (int64_t k = 0; k < c.ncells; k++) /* life_cart.c:106-109 */
-            grid[wrapi(c.cells[2 * k + 1], c.ny) * c.nx + wrapi(c.cells[2 * k], c.nx)] = 1;
-        rc = life_dev_upload(d, grid);
+        rc = life_dev_upload(d, c.grid);
     }
     if (rc) die("init", rc);
-    free(c.cells);
+    free(c.grid);
+    c.grid = NULL;
 
     /* life_cart.c:62-80: the timer starts after init and covers the frame
      * collects + VTK writes and every generation. */

@@ -124,3 +124,33 @@ def test_gather_vtk_equals_host_format(gpu, oracle, kernel, nx, ny, shards):
         life.upload(g0)
         life.step(3)
         assert life.gather_vtk() == gpu.vtk_bytes(life.gather())
+
+
+def test_driver_large_cfg_parallel_parse(gpu, tmp_path):
+    """A multi-MB .cfg goes through the driver's mapped, multi-threaded parser
+    (line-aligned chunks): frame 0 == the numpy loader's grid, with negative
+    and out-of-range coordinates wrapped; one token per line (pairs split
+    across chunk boundaries) takes the sequential pairing path; a malformed
+    token is an error (the reference's fscanf loop would spin forever)."""
+    rng = np.random.default_rng(3)
+    n = 1536
+    ys, xs = np.nonzero(rng.random((n, n)) < 0.5)
+    xs = xs + n * rng.integers(-2, 3, xs.size)  # periodic wrap on load (life_cart.c:106-109)
+    head = f"2\n1\n{n} {n}\n"
+    for name, body in (("lines", "".join(f"{x} {y}\n" for x, y in zip(xs, ys))),
+                       ("tokens", "".join(f"{x}\n{y}\n" for x, y in zip(xs, ys)))):
+        p = tmp_path / f"{name}.cfg"
+        p.write_text(head + body)
+        assert p.stat().st_size > 8 << 20  # several parser threads
+        run = tmp_path / name
+        run.mkdir()
+        r = subprocess.run([DRIVER, str(p), "--format", "bits", "--steps", "1"], cwd=run, capture_output=True,
+                           text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        want = gpu.load_cfg(str(p))[2]
+        _, got = gpu.load_bits(str(run / "vtk" / "life_000000.bits"))
+        np.testing.assert_array_equal(got, want)
+    bad = tmp_path / "bad.cfg"
+    bad.write_text(head + "1 2\n3 x4\n")
+    r = subprocess.run([DRIVER, str(bad)], cwd=tmp_path, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "cannot read config" in r.stderr
