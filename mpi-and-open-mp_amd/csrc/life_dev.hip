@@ -13,6 +13,7 @@
 // ring runs first, the halo exchange of the NEW state runs on the comm stream
 // while the interior kernel runs on the compute stream.
 #include <rccl/rccl.h>
+#include <algorithm>
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
@@ -110,7 +111,9 @@ struct life_dev {
 
 namespace {
 
-life::Wrap wrap_of(const life_dev *d) { return life::Wrap{d->dims[0] == 1, d->dims[1] == 1}; }
+// The shard wraps x itself (the x-apron is filled by launch_wrap_columns).
+bool self_wrap_x(const life_dev *d) { return life::self_wrap_x(d->shards[0].lay, d->dims[0]); }
+life::Wrap wrap_of(const life_dev *d) { return life::Wrap{d->dims[0] == 1 && !self_wrap_x(d), d->dims[1] == 1}; }
 
 int shard_alloc(life_dev *d, Shard &s) {
     HIPCHK(hipSetDevice(s.device));
@@ -204,8 +207,17 @@ int run_phase(life_dev *d, int phase, int which_rel, bool on_comm) {
     auto stream_of = [&](Shard &s) { return on_comm ? s.comm_stream : s.stream; };
     auto buf_of = [&](Shard &s) { return s.buf[s.cur ^ which_rel]; };
     // An axis that is not partitioned (dims[d] == 1) has no halo: the stencil
-    // wraps it itself (life_kernels.hip, row_ptr / WRAPX).
-    if (d->dims[phase] == 1) return LIFE_OK;
+    // wraps it itself (life_kernels.hip, row_ptr / WRAPX), or, for a temporal
+    // layout whose width is not a multiple of 32, the shard copies its own
+    // edge columns into its x-apron.
+    if (d->dims[phase] == 1) {
+        if (phase == 0 && self_wrap_x(d))
+            for (Shard &s : d->shards) {
+                HIPCHK(hipSetDevice(s.device));
+                HIPCHK(life::launch_wrap_columns(s.lay, buf_of(s), stream_of(s)));
+            }
+        return LIFE_OK;
+    }
     if (phase == 0)
         for (Shard &s : d->shards) {
             HIPCHK(hipSetDevice(s.device));
@@ -366,15 +378,14 @@ int launch_tiles(life_dev *d, Shard &s, const life::TileRegion *r, int nreg, int
     if (t) {
         HIPCHK(hipEventRecord(t->b, st));
         const life::TileGeom g = life::tile_geom(s.lay);
-        const int64_t W = s.lay.w / 32;
         for (int k = 0; k < nreg; k++) {
-            const int64_t wa = r[k].tx0 * g.words, wb = r[k].tx1 * g.words < W ? r[k].tx1 * g.words : W;
-            const int64_t ya = r[k].ty0 * g.rows, yb = r[k].ty1 * g.rows < s.lay.h ? r[k].ty1 * g.rows : s.lay.h;
-            if (wb > wa && yb > ya) {
+            const int64_t xa = r[k].tx0 * g.words * 32, xb = std::min(r[k].tx1 * g.words * 32, s.lay.w);
+            const int64_t ya = r[k].ty0 * g.rows, yb = std::min(r[k].ty1 * g.rows, s.lay.h);
+            if (xb > xa && yb > ya) {
                 // compulsory HBM bytes of the launch: each owned cell's bit is
                 // read once and written once per m-generation pass (0.25 B),
                 // not once per generation -- that is the point of the blocking
-                const double cells = (double)(wb - wa) * 32.0 * (double)(yb - ya);
+                const double cells = (double)(xb - xa) * (double)(yb - ya);
                 d->acc_bytes += cells * (s.lay.kernel == LIFE_KERNEL_BIT ? 0.25 : 2.0);
                 d->acc_updates += cells * (double)m;
             }
@@ -396,13 +407,17 @@ int join_streams(Shard &s) {
     return LIFE_OK;
 }
 
-// m <= K generations of the temporally blocked bit stencil on every shard,
-// then one K-deep halo exchange.  Partitioned shards: the boundary ring tiles
+// m <= K generations of the temporally blocked stencil on every shard, then
+// one K-deep halo exchange.  Partitioned shards: the boundary ring tiles
 // (one multi-region launch) run on the compute stream, the exchange of their
 // new state on the comm stream, and the interior tiles concurrently on the
-// second compute stream.
+// second compute stream.  The ring holds every tile that produces a cell the
+// exchange sends: rows [0, K) and [h-K, h) (two tile rows at each end when the
+// last tile row is shorter than K), columns [0, 32) and [w-32, w) (the tile
+// column of word (w-32)/32 onwards when w % 32 != 0).  A self-wrapped x axis
+// (life::self_wrap_x) counts as partitioned: its "exchange" is the column copy.
 int generation_block(life_dev *d, int m) {
-    const bool rx = d->dims[0] > 1, ry = d->dims[1] > 1;
+    const bool rx = d->dims[0] > 1 || self_wrap_x(d), ry = d->dims[1] > 1;
     if (!(rx || ry)) {
         for (Shard &s : d->shards) {
             HIPCHK(hipSetDevice(s.device));
@@ -416,24 +431,30 @@ int generation_block(life_dev *d, int m) {
     for (Shard &s : d->shards) {
         HIPCHK(hipSetDevice(s.device));
         const life::TileGeom g = life::tile_geom(s.lay);
-        const int64_t TX = g.ntx, TY = g.nty;
-        const int64_t ra = ry ? 1 : 0, rb = ry ? TY - 1 : TY;
+        const int64_t TX = g.ntx, TY = g.nty, K = s.lay.generations_per_exchange;
+        // tile rows [0, ra) and [rb, TY), tile columns [0, ca) and [cb, TX)
+        int64_t ra = 0, rb = TY, ca = 0, cb = TX;
+        if (ry) {
+            ra = std::min((K + g.rows - 1) / g.rows, TY);
+            rb = std::max(std::min((s.lay.h - K) / g.rows, TY), ra);
+        }
+        if (rx) {
+            ca = 1;
+            cb = std::max(std::min(((s.lay.w - 32) / 32) / g.words, TX), ca);
+        }
         life::TileRegion ring[4];
         int n = 0;
-        if (ry) {
-            ring[n++] = life::TileRegion{0, TX, 0, 1};
-            if (TY > 1) ring[n++] = life::TileRegion{0, TX, TY - 1, TY};
-        }
-        if (rx && rb > ra) {
-            ring[n++] = life::TileRegion{0, 1, ra, rb};
-            if (TX > 1) ring[n++] = life::TileRegion{TX - 1, TX, ra, rb};
+        if (ra > 0) ring[n++] = life::TileRegion{0, TX, 0, ra};
+        if (rb < TY) ring[n++] = life::TileRegion{0, TX, rb, TY};
+        if (rb > ra) {
+            if (ca > 0) ring[n++] = life::TileRegion{0, ca, ra, rb};
+            if (cb < TX) ring[n++] = life::TileRegion{cb, TX, ra, rb};
         }
         CHK(launch_tiles(d, s, ring, n, m, false, s.stream));
         HIPCHK(hipEventRecord(s.ev_ring, s.stream));
         HIPCHK(hipStreamWaitEvent(s.comm_stream, s.ev_ring, 0));
-        const int64_t ua = rx ? 1 : 0, ub = rx ? TX - 1 : TX;
-        const life::TileRegion inner{ua, ub, ra, rb};
-        if (rb > ra && ub > ua) CHK(launch_tiles(d, s, &inner, 1, m, true, s.stream2));
+        const life::TileRegion inner{ca, cb, ra, rb};
+        if (rb > ra && cb > ca) CHK(launch_tiles(d, s, &inner, 1, m, true, s.stream2));
     }
     CHK(exchange(d, 1, true));
     for (Shard &s : d->shards) {
@@ -706,7 +727,9 @@ int life_dev_step(life_dev *d, int64_t generations) {
         constexpr int64_t kChunk = 1 << 20;  // generations per resident launch
         for (int64_t g = 0; g < generations; g += kChunk)
             CHK(step_small(d, generations - g < kChunk ? generations - g : kChunk));
-        return LIFE_OK;
+        // the LDS kernel wraps inside the CU and leaves the buffer's aprons
+        // stale: refresh them (a self-wrapped x axis; no-op otherwise)
+        return exchange(d, 0, false);
     }
     if (temporal(d)) {
         const int K = d->shards[0].lay.generations_per_exchange;

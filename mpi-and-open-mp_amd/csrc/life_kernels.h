@@ -89,6 +89,13 @@ hipError_t launch_pack_columns(const life_layout &L, const uint8_t *buf, uint8_t
                                hipStream_t s);
 hipError_t launch_unpack_columns(const life_layout &L, uint8_t *buf, const uint8_t *stage,
                                  hipStream_t s);
+// Temporal layouts: a periodic x axis inside one shard is wrapped by the
+// stencil (whole words) when w % 32 == 0; otherwise the shard fills its own
+// 32-cell aprons from its own columns (launch_wrap_columns, needs w >= 32).
+inline bool self_wrap_x(const life_layout &L, int dims0) {
+    return L.xapron == 32 && dims0 == 1 && L.w % 32 != 0;
+}
+hipError_t launch_wrap_columns(const life_layout &L, uint8_t *buf, hipStream_t s);
 
 // Dense w*h byte block (row pitch w) <-> padded encoded buffer.
 hipError_t launch_import_block(const life_layout &L, const uint8_t *dense, uint8_t *buf,

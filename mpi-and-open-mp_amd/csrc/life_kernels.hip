@@ -640,7 +640,30 @@ __device__ __forceinline__ void set_cell(uint8_t *row, int64_t xoff, int64_t x, 
 }
 
 // Column halo staging.  Cell columns (xapron == 1): one byte 0/1 per row.
-// Word columns (bit encoding, xapron == 32): the whole dword per row.
+// 32-cell columns (temporal layouts, xapron == 32): the bit encoding sends
+// one dword per row and side, the byte encoding 32 bytes.  The left column
+// (cells [0, 32)) is word 0; the right one (cells [w-32, w)) and the right
+// apron (cells [w, w+32)) straddle two words when w % 32 != 0: a funnel shift
+// on the way out, a bit merge that keeps the owned cells on the way in.
+__device__ __forceinline__ uint32_t right_column_bits(const uint32_t *wd, int64_t w) {
+    const int64_t x = w - 32;  // w >= 32
+    return __builtin_amdgcn_alignbit(wd[(w - 1) >> 5], wd[x >> 5], (uint32_t)(x & 31));
+}
+__device__ __forceinline__ void put_right_apron_bits(uint32_t *wd, int64_t w, uint32_t v) {
+    const uint32_t s = (uint32_t)(w & 31);
+    uint32_t *q = wd + (w >> 5);
+    if (s == 0) {
+        q[0] = v;
+        return;
+    }
+    q[0] = (q[0] & ((1u << s) - 1u)) | (v << s);
+    q[1] = v >> (32u - s);  // cells beyond w+31: never read as owned
+}
+__device__ __forceinline__ void copy32(uint8_t *dst, const uint8_t *src) {
+    // byte-cell columns need not be 4-byte aligned (w % 4 != 0)
+    for (int k = 0; k < 32; ++k) dst[k] = src[k];
+}
+
 __global__ void pack_columns_kernel(const uint8_t *buf, int64_t pitch, int64_t ya, int64_t xoff, int64_t w,
                                     int64_t h, int64_t xa, uint8_t *stage, bool bit) {
     const int64_t y = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -648,17 +671,16 @@ __global__ void pack_columns_kernel(const uint8_t *buf, int64_t pitch, int64_t y
     const uint8_t *row = buf + (y + ya) * pitch;
     if (xa == 32 && bit) {
         const uint32_t *wd = reinterpret_cast<const uint32_t *>(row + xoff);
-        reinterpret_cast<uint32_t *>(stage)[y] = wd[(w - 32) >> 5];
+        reinterpret_cast<uint32_t *>(stage)[y] = right_column_bits(wd, w);
         reinterpret_cast<uint32_t *>(stage)[h + y] = wd[0];
         return;
     }
     if (xa == 32) {  // 32 byte cells per row and side
-        const uint4 *r = reinterpret_cast<const uint4 *>(row + xoff + w - 32), *l = reinterpret_cast<const uint4 *>(row + xoff);
-        uint4 *st = reinterpret_cast<uint4 *>(stage);
-        st[2 * y] = r[0];
-        st[2 * y + 1] = r[1];
-        st[2 * (h + y)] = l[0];
-        st[2 * (h + y) + 1] = l[1];
+        copy32(stage + 32 * y, row + xoff + w - 32);
+        const uint4 *l = reinterpret_cast<const uint4 *>(row + xoff);
+        uint4 *st = reinterpret_cast<uint4 *>(stage + 32 * (h + y));
+        st[0] = l[0];
+        st[1] = l[1];
         return;
     }
     stage[y] = (uint8_t)get_cell(row, xoff, w - 1, bit);
@@ -673,20 +695,38 @@ __global__ void unpack_columns_kernel(uint8_t *buf, int64_t pitch, int64_t ya, i
     if (xa == 32 && bit) {
         uint32_t *wd = reinterpret_cast<uint32_t *>(row + xoff);
         wd[-1] = reinterpret_cast<const uint32_t *>(stage)[y];
-        wd[w >> 5] = reinterpret_cast<const uint32_t *>(stage)[h + y];
+        put_right_apron_bits(wd, w, reinterpret_cast<const uint32_t *>(stage)[h + y]);
         return;
     }
     if (xa == 32) {
-        uint4 *l = reinterpret_cast<uint4 *>(row + xoff - 32), *r = reinterpret_cast<uint4 *>(row + xoff + w);
-        const uint4 *st = reinterpret_cast<const uint4 *>(stage);
-        l[0] = st[2 * y];
-        l[1] = st[2 * y + 1];
-        r[0] = st[2 * (h + y)];
-        r[1] = st[2 * (h + y) + 1];
+        uint4 *l = reinterpret_cast<uint4 *>(row + xoff - 32);
+        const uint4 *st = reinterpret_cast<const uint4 *>(stage + 32 * y);
+        l[0] = st[0];
+        l[1] = st[1];
+        copy32(row + xoff + w, stage + 32 * (h + y));
         return;
     }
     set_cell(row, xoff, -1, stage[y] ? 1u : 0u, bit);
     set_cell(row, xoff, w, stage[h + y] ? 1u : 0u, bit);
+}
+
+// Periodic x inside one shard of a temporal layout whose width is not a
+// multiple of 32 (the stencil's WRAPX reads whole words): the shard is its own
+// left and right neighbour, so the aprons are filled from its own columns.
+__global__ void wrap_columns_kernel(uint8_t *buf, int64_t pitch, int64_t ya, int64_t xoff, int64_t w, int64_t h,
+                                    bool bit) {
+    const int64_t y = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (y >= h) return;
+    uint8_t *row = buf + (y + ya) * pitch;
+    if (bit) {
+        uint32_t *wd = reinterpret_cast<uint32_t *>(row + xoff);
+        const uint32_t l = wd[0], r = right_column_bits(wd, w);
+        wd[-1] = r;
+        put_right_apron_bits(wd, w, l);
+        return;
+    }
+    copy32(row + xoff - 32, row + xoff + w - 32);
+    copy32(row + xoff + w, row + xoff);
 }
 
 // One thread per 16-byte unit of an owned row: dense (row pitch w) -> padded.
@@ -997,7 +1037,7 @@ TileGeom tile_geom(const life_layout &L) {
     TileGeom g;
     g.words = 62;
     g.rows = (int64_t)kStackWaves * temporal_rows(is_bit(L)) - 2 * (int64_t)L.generations_per_exchange;
-    g.ntx = (L.w / 32 + g.words - 1) / g.words;
+    g.ntx = ((L.w + 31) / 32 + g.words - 1) / g.words;
     g.nty = (L.h + g.rows - 1) / g.rows;
     return g;
 }
@@ -1012,7 +1052,7 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
     a.out = out;
     a.pitch = L.pitch;
     a.xoff = L.xoff;
-    a.W = L.w / 32;
+    a.W = (L.w + 31) / 32;  // the last word may be partial: its upper cells are the right apron
     a.h = L.h;
     a.ya = L.yapron;
     a.m = m;
@@ -1069,6 +1109,12 @@ hipError_t launch_small(const life_layout &L, const uint8_t *in, uint8_t *out, i
 hipError_t launch_pack_columns(const life_layout &L, const uint8_t *buf, uint8_t *stage, hipStream_t s) {
     pack_columns_kernel<<<blocks_for(L.h, 256), 256, 0, s>>>(buf, L.pitch, L.yapron, L.xoff, L.w, L.h, L.xapron,
                                                               stage, is_bit(L));
+    return hipGetLastError();
+}
+
+hipError_t launch_wrap_columns(const life_layout &L, uint8_t *buf, hipStream_t s) {
+    if (L.xapron != 32 || L.w < 32) return hipErrorInvalidValue;
+    wrap_columns_kernel<<<blocks_for(L.h, 256), 256, 0, s>>>(buf, L.pitch, L.yapron, L.xoff, L.w, L.h, is_bit(L));
     return hipGetLastError();
 }
 

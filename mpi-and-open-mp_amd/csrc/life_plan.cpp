@@ -53,15 +53,15 @@ static int temporal_depth(int kernel) {
     return kernel == LIFE_KERNEL_BIT ? kbit : kbyte;
 }
 
-// The temporally blocked stencil (either encoding) exchanges whole 32-cell words
-// in x and K = temporal_depth() rows in y, and wraps a non-partitioned x axis
-// at word granularity: every block width must be a multiple of 32, and a
-// partitioned y axis needs blocks at least as tall as the apron it feeds.
+// The temporally blocked stencil (either encoding) keeps 32-cell x-aprons
+// and K-row y-aprons: every block must be at least 32 cells wide (a neighbour,
+// or the shard itself when x wraps inside it, fills the 32 apron columns) and,
+// on a partitioned y axis, at least K rows tall.
 static bool temporal_ok(int64_t nx, int64_t ny, int dims0, int dims1, int K) {
     for (int k = 0; k < dims0; k++) {
         int64_t s, e;
         life_decomposition(nx, dims0, k, &s, &e);
-        if ((e - s) % 32 != 0) return false;
+        if (e - s < 32) return false;
     }
     if (dims1 > 1)
         for (int k = 0; k < dims1; k++) {
@@ -99,8 +99,9 @@ int life_layout_query(int64_t nx, int64_t ny, int dims0, int dims1, int rank, in
     out->units = (out->w + cells_per_unit - 1) / cells_per_unit;
     out->xoff = kXoff;
     // room for the last unit, the right apron (cell, word, or 32 byte cells)
-    // and the right extra dword
-    out->pitch = round_up(kXoff + 16 * out->units + (temporal && kernel == LIFE_KERNEL_BYTE ? 32 : 16), 256);
+    // and the right extra dword; the temporal byte stencil reads whole 32-byte
+    // words up to the one holding cell w+31
+    out->pitch = round_up(kXoff + 16 * out->units + (temporal && kernel == LIFE_KERNEL_BYTE ? 64 : 16), 256);
     out->rows = out->h + 2 * out->yapron;
     return LIFE_OK;
 }

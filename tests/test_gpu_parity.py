@@ -74,11 +74,12 @@ def test_byte_equals_bit_long(gpu, oracle, nx):
     np.testing.assert_array_equal(out["bit"], oracle.life_run(g0, gens, threads=4))
 
 
-@pytest.mark.parametrize("kernel,nx,launches,gens", [("bit", 4096, 2, 40), ("bit", 4016, 13, 13),
-                                                     ("byte", 4096, 2, 40), ("byte", 4016, 13, 13)])
+@pytest.mark.parametrize("kernel,nx,launches,gens", [("bit", 4096, 2, 40), ("bit", 31, 13, 13),
+                                                     ("byte", 4096, 2, 40), ("byte", 31, 13, 13)])
 def test_timing_stats(gpu, kernel, nx, launches, gens):
-    """One timed launch per generation (one-generation kernels) or per up to
-    8 generations (temporal bit kernel).  Bytes are the compulsory HBM
+    """One timed launch per generation (one-generation kernels: a block
+    narrower than the 32-cell apron) or per up to K generations (temporal
+    kernels).  Bytes are the compulsory HBM
     traffic: 0.25 B (bit) / 2 B (byte) per cell per LAUNCH; cell-updates are
     cells x generations; VALU lane-ops are modelled for the temporal kernel
     only (13 per register row per generation: the 14th op, the right
@@ -105,10 +106,12 @@ def test_timing_stats(gpu, kernel, nx, launches, gens):
 # ---------------------------------------------------------------- temporal blocking (bit)
 @pytest.mark.parametrize("kernel", ["bit", "byte"])
 @pytest.mark.parametrize("nx,ny", [(32, 1), (32, 5), (64, 64), (96, 33), (2048, 100), (1024, 1000), (4096, 48),
-                                   (32, 200), (1984, 130), (2016, 7)])
+                                   (32, 200), (1984, 130), (2016, 7),
+                                   # widths not a multiple of 32: the shard wraps its own x-aprons
+                                   (33, 9), (63, 64), (500, 500), (1000, 37), (4016, 130), (1985, 3), (2047, 200)])
 def test_temporal_single_shard(gpu, oracle, kernel, nx, ny):
-    """Word-aligned widths take the temporally blocked kernel (up to K = 16
-    generations per launch); runs of 1, 7, 8, 9, 20 and 40 generations."""
+    """Blocks at least 32 cells wide take the temporally blocked kernel (up to
+    K generations per launch); runs of 1, 7, 8, 9, 20 and 40 generations."""
     assert gpu.layout_query(nx, ny, (1, 1), 0, kernel).generations_per_exchange == gpu.TEMPORAL_DEPTH[kernel]
     g0 = oracle.fill_random(nx, ny, seed=nx + 3 * ny, density=0.5)
     with gpu.Life(nx, ny, kernel=kernel, small_grid=False) as life:
@@ -124,6 +127,8 @@ def test_temporal_single_shard(gpu, oracle, kernel, nx, ny):
 @pytest.mark.parametrize("nx,ny,shards,dims", [
     (256, 64, 4, (2, 2)), (512, 80, 8, (4, 2)), (64, 80, 4, (1, 4)), (256, 9, 4, (4, 1)), (64, 20, 2, (2, 1)),
     (96, 32, 6, (3, 2)), (4096, 4096, 4, (2, 2)), (8192, 200, 8, (4, 2)), (2048, 1100, 2, (1, 2)),
+    # block widths not a multiple of 32 (remainder rule, straddling columns)
+    (500, 500, 2, (2, 1)), (500, 300, 8, (4, 2)), (100, 64, 6, (3, 2)), (1000, 70, 4, (2, 2)), (2047, 90, 2, (1, 2)),
 ])
 @pytest.mark.parametrize("kernel", ["bit", "byte"])
 def test_temporal_multi_shard_local(gpu, oracle, kernel, nx, ny, shards, dims):
