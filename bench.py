@@ -168,6 +168,7 @@ def main():
 
     if rank == 0:
         cells = float(nx) * float(ny) * a.steps
+        bpu = 0.25 if a.kernel == "bit" else 2.0  # algorithmic HBM bytes per cell-update
         value = cells / elapsed / 1e9
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
         gens_per_launch = updates_per_launch / (bytes_per_launch / (0.25 if a.kernel == "bit" else 2.0)) \
@@ -201,7 +202,12 @@ def main():
                          # advances K > 1 generations per pass over HBM
                          "per_generation_equivalent_GBps": round(
                              updates_per_launch * (0.25 if a.kernel == "bit" else 2.0) / (avg_ms * 1e-3) / 1e9, 1)
-                         if avg_ms > 0 else 0.0},
+                         if avg_ms > 0 else 0.0,
+                         # the north-star question "% of HBM roofline" in cell-update terms: the
+                         # rate a one-generation-per-HBM-pass kernel would reach at the HBM peak on
+                         # n_gpus GPUs (8 TB/s / 0.25 B or 2 B per update), and value against it
+                         "hbm_bound_cell_rate": round(n_gpus * HBM_PEAK_GBS / bpu, 1),
+                         "cell_rate_vs_hbm_bound": round(value / (n_gpus * HBM_PEAK_GBS / bpu), 4)},
         }
         if valu_per_launch > 0 and avg_ms > 0:
             # the temporally blocked kernel is VALU-issue bound, not HBM bound

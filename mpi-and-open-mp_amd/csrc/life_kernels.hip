@@ -355,8 +355,19 @@ __device__ __forceinline__ uint32_t right_or_zero(uint32_t v) {
 __device__ __forceinline__ uint32_t bperm(int addr, uint32_t v) {
     return (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)v);
 }
-__device__ __forceinline__ void bit_hsum(uint32_t v, uint32_t &s0, uint32_t &s1) {
-#if LIFE_HSUM_MODE == 0
+// Mode 3: both neighbour words through a per-wave LDS row (one ds_write_b32,
+// one ds_read2_b32): LDS operations of one wave execute in issue order, so the
+// read sees the write without a wait; the signal fences keep the compiler
+// from reordering the row's LDS accesses (slot[0] and slot[65] stay 0).
+__device__ __forceinline__ void bit_hsum(uint32_t v, uint32_t &s0, uint32_t &s1, uint32_t *slot) {
+#if LIFE_HSUM_MODE == 3
+    const int lane = (int)__lane_id();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    slot[lane + 1] = v;
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    const uint32_t l = slot[lane], r = slot[lane + 2];
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+#elif LIFE_HSUM_MODE == 0
     const uint32_t l = left_or_zero(v), r = right_or_zero(v);
 #else
     const int lane = (int)__lane_id();
@@ -396,6 +407,13 @@ __global__ __launch_bounds__(64 * kStackWaves, 4) void tstep_kernel(TArgs a) {  
     const int lane = threadIdx.x & 63;
     // wave index: uniform, so every row address below is scalar (SALU) math
     const int wi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#if LIFE_HSUM_MODE == 3
+    __shared__ uint32_t rowx[NW][66];  // per-wave neighbour row, zero pads at 0 and 65
+    uint32_t *slot = rowx[wi];
+    if (lane < 2) slot[lane * 65] = 0u;
+#else
+    uint32_t *slot = nullptr;
+#endif
     const int64_t nwg = a.first[a.nreg];
     if ((int64_t)blockIdx.x >= nwg) return;  // whole workgroup
 #if LIFE_XCD_ORDER
@@ -464,8 +482,8 @@ __global__ __launch_bounds__(64 * kStackWaves, 4) void tstep_kernel(TArgs a) {  
     for (int g = 0; g < a.m; ++g) {
         const int par = g & 1;
         uint32_t t0, t1, b0, b1;
-        bit_hsum(v[0], t0, t1);
-        bit_hsum(v[R - 1], b0, b1);
+        bit_hsum(v[0], t0, t1, slot);
+        bit_hsum(v[R - 1], b0, b1, slot);
         xch[par][wi][0][lane] = t0;
         xch[par][wi][1][lane] = t1;
         xch[par][wi][2][lane] = b0;
@@ -484,7 +502,7 @@ __global__ __launch_bounds__(64 * kStackWaves, 4) void tstep_kernel(TArgs a) {  
         // rows 1 .. R-2 need only this wave's rows: they run while the LDS
         // reads are in flight
         uint32_t p0 = t0, p1 = t1, c0, c1;
-        bit_hsum(v[1], c0, c1);
+        bit_hsum(v[1], c0, c1, slot);
         const uint32_t h10 = c0, h11 = c1;
 #pragma unroll
         for (int r = 1; r < R - 1; ++r) {
@@ -493,7 +511,7 @@ __global__ __launch_bounds__(64 * kStackWaves, 4) void tstep_kernel(TArgs a) {  
                 n0 = b0;
                 n1 = b1;
             } else {
-                bit_hsum(v[r + 1], n0, n1);
+                bit_hsum(v[r + 1], n0, n1, slot);
             }
             v[r] = BitEnc::rule1(p0, p1, c0, c1, n0, n1, v[r]);
             p0 = c0;

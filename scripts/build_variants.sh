@@ -17,6 +17,7 @@ for v in "$@"; do
         hsum0) build hsum0 -DLIFE_HSUM_MODE=0 ;;
         hsum1) build hsum1 -DLIFE_HSUM_MODE=1 ;;
         hsum2) build hsum2 -DLIFE_HSUM_MODE=2 ;;
+        hsum3) build hsum3 -DLIFE_HSUM_MODE=3 ;;
         nw16) build nw16 -DLIFE_STACK_WAVES=16 ;;
         nw4) build nw4 -DLIFE_STACK_WAVES=4 ;;
         xcd) build xcd -DLIFE_XCD_ORDER=1 ;;
