@@ -28,7 +28,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "mpi-and-open-mp_amd"))
 
-if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+if int(os.environ.get("WORLD_SIZE", "1")) > 1 or "--rank-mode" in sys.argv:
     # torch bundles its own HIP runtime and links it by its unversioned name;
     # loading torch FIRST makes liblife_mi355x.so bind to that same runtime
     # (SONAME libamdhip64.so.7) instead of a second copy from /opt/rocm.
@@ -58,6 +58,8 @@ def parse():
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline sample budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--rank-mode", action="store_true",
+                   help="one-process-per-GPU set-up (gloo bootstrap, RCCL communicator) even at world 1")
     return p.parse_args()
 
 
@@ -112,7 +114,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    rank_mode = world > 1 or a.rank_mode
+    if rank_mode:
         import torch.distributed as dist  # noqa: F811
 
         dist.init_process_group("gloo")
@@ -128,7 +131,7 @@ def main():
         grid = None
         workload = f"random 50% {a.size}^2 per GPU, global {nx}x{ny} (configs[4] weak scaling)"
 
-    if world > 1:
+    if rank_mode:
         uid = [lm.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         life = lm.Life.for_rank(nx, ny, rank, world, uid[0], local_rank, kernel=a.kernel, dims=dims)

@@ -132,7 +132,9 @@ int life_dev_create_ex(int64_t nx, int64_t ny, int nshards, int dims0, int dims1
 
 /* One-process-per-GPU mode (torchrun / mpirun style): this process owns the
  * single shard `rank` of `world` on `device`; `unique_id` (128 bytes) comes
- * from life_get_unique_id() on rank 0, broadcast by the caller. */
+ * from life_get_unique_id() on rank 0, broadcast by the caller (required when
+ * world > 1; with world == 1 it is optional and, if given, still builds a
+ * one-rank RCCL communicator, used by the census all-reduce). */
 int life_get_unique_id(uint8_t unique_id[128]);
 int life_dev_create_rank(int64_t nx, int64_t ny, int kernel, int rank, int world, int dims0,
                          int dims1, const uint8_t unique_id[128], int device, life_dev **out);

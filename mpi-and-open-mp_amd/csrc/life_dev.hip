@@ -625,7 +625,10 @@ int life_dev_create_rank(int64_t nx, int64_t ny, int kernel, int rank, int world
     d->rank_mode = true;
     d->transport = LIFE_XPORT_RCCL;
     int rc = create_common(d, {rank}, {device});
-    if (rc == LIFE_OK && world > 1) {
+    // A communicator whenever the caller hands a unique id, world 1 included
+    // (then only the census all-reduce uses it; that is how a one-GPU box
+    // exercises RCCL initialisation in the torchrun process set-up).
+    if (rc == LIFE_OK && (world > 1 || unique_id)) {
         if (!unique_id) {
             rc = LIFE_EINVAL;
         } else {
@@ -855,7 +858,7 @@ static int census(life_dev *d, unsigned long long out[2]) {
         HIPCHK(hipSetDevice(s.device));
         HIPCHK(hipMemsetAsync(s.d_count, 0, 2 * sizeof(unsigned long long), s.stream));
         HIPCHK(life::launch_census(s.lay, d->nx, s.buf[s.cur], s.d_count, s.stream));
-        if (d->rank_mode && d->world > 1)
+        if (d->rank_mode && s.comm)
             NCCLCHK(ncclAllReduce(s.d_count, s.d_count, 2, ncclUint64, ncclSum, s.comm, s.stream));
         HIPCHK(hipMemcpyAsync(s.h_count, s.d_count, 2 * sizeof *s.h_count, hipMemcpyDeviceToHost, s.stream));
         HIPCHK(hipStreamSynchronize(s.stream));  // pinned destination
