@@ -53,6 +53,24 @@ void life_decomposition(int64_t n, int p, int k, int64_t *start, int64_t *stop);
  * dims[0] >= dims[1], as balanced as possible. 2->{2,1}, 4->{2,2}, 8->{4,2}. */
 void life_dims_create(int n, int dims[2]);
 
+/* Partition shape for n shards of an nx x ny grid (the 1-D
+ * row strips of 3-life/4-life/5-gather vs the 2-D blocks of 6-cartesian).
+ * CART: life_dims_create (life_cart.c:117-118).  ROWS: {1, n}, horizontal
+ * strips (5-gather/life_mpi.c:96-99 cuts y the same way): every halo message is
+ * a run of whole padded rows, sent straight from the buffer with no pack
+ * kernel.  COLS: {n, 1}.  AUTO: ROWS when every strip is at least
+ * LIFE_AUTO_MIN_STRIP_ROWS tall, else CART -- measured
+ * on MI355X with the LOCAL transport at 65536^2 per shard (DESIGN.md §6,
+ * profiles/r01/partition_sweep.jsonl), row strips cost the owning GPU 0-6 %
+ * less per generation than 2-D blocks with either encoding.  Returns
+ * LIFE_EINVAL for n < 1, an unknown policy or a shape with empty blocks. */
+#define LIFE_PARTITION_CART 0
+#define LIFE_PARTITION_ROWS 1
+#define LIFE_PARTITION_COLS 2
+#define LIFE_PARTITION_AUTO 3
+#define LIFE_AUTO_MIN_STRIP_ROWS 1024
+int life_dims_choose(int64_t nx, int64_t ny, int n, int policy, int dims[2]);
+
 /* One halo-exchange operation of a shard (replaces exchange_columns /
  * exchange_rows / exchange_corners, life_cart.c:225-279, and the 1-D ring
  * exchange of 5-gather/life_mpi.c:181-191).  Coordinates are the shard's

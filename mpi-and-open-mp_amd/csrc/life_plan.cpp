@@ -37,6 +37,25 @@ void life_dims_create(int n, int dims[2]) {
     dims[1] = d1;
 }
 
+int life_dims_choose(int64_t nx, int64_t ny, int n, int policy, int dims[2]) {
+    if (!dims || n < 1 || nx <= 0 || ny <= 0) return LIFE_EINVAL;
+    switch (policy) {
+    case LIFE_PARTITION_CART: life_dims_create(n, dims); break;
+    case LIFE_PARTITION_ROWS: dims[0] = 1, dims[1] = n; break;
+    case LIFE_PARTITION_COLS: dims[0] = n, dims[1] = 1; break;
+    case LIFE_PARTITION_AUTO:
+        // the shortest strip (the decomposition remainder goes to the last)
+        if (ny / n >= LIFE_AUTO_MIN_STRIP_ROWS)
+            dims[0] = 1, dims[1] = n;
+        else
+            life_dims_create(n, dims);
+        break;
+    default: return LIFE_EINVAL;
+    }
+    if (nx < dims[0] || ny < dims[1]) return LIFE_EINVAL;
+    return LIFE_OK;
+}
+
 // Generations per halo exchange of the temporally blocked layout, per
 // encoding: LIFE_TEMPORAL_DEPTH (bit) / LIFE_TEMPORAL_DEPTH_BYTE, or 16 / 24
 // / 32 from the environment variables of the same names (read once; every rank

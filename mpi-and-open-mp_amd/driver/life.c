@@ -12,6 +12,9 @@
  *   --gpus N          shards driven by this process (one per GPU; with more
  *                     shards than GPUs they share devices, LOCAL transport)
  *   --kernel byte|bit cell encoding (default bit)
+ *   --partition cart|rows|cols|auto   shard shape (life_dims_choose; default
+ *                     cart = MPI_Dims_create as life_cart.c:117-118; rows =
+ *                     the 1-D strips of 3-life/5-gather; the grid is the same)
  *   --nx N --ny N --steps N --save-steps N   override the .cfg header
  *   --random SEED[,DENSITY]                  device-side random init instead
  *                                            of the .cfg cells (no file needed)
@@ -266,6 +269,7 @@ static int load_bits(const char *path, int64_t *nx, int64_t *ny, uint8_t **grid)
 int main(int argc, char **argv) {
     const char *cfg_path = NULL, *resume = NULL;
     int gpus = 1, kernel = LIFE_KERNEL_BIT, vtk = 1, live = 0, have_random = 0, bits = 0;
+    int partition = LIFE_PARTITION_CART;
     long long o_nx = -1, o_ny = -1, o_steps = -1, o_save = -1;
     unsigned long long seed = 0;
     double density = 0.5;
@@ -273,6 +277,14 @@ int main(int argc, char **argv) {
         const char *s = argv[a];
         const int more = a + 1 < argc;
         if (!strcmp(s, "--gpus") && more) gpus = atoi(argv[++a]);
+        else if (!strcmp(s, "--partition") && more) {
+            const char *p = argv[++a];
+            partition = !strcmp(p, "cart")   ? LIFE_PARTITION_CART
+                        : !strcmp(p, "rows") ? LIFE_PARTITION_ROWS
+                        : !strcmp(p, "cols") ? LIFE_PARTITION_COLS
+                        : !strcmp(p, "auto") ? LIFE_PARTITION_AUTO
+                                             : -1;
+        }
         else if (!strcmp(s, "--kernel") && more) {
             const char *k = argv[++a];
             kernel = !strcmp(k, "byte") ? LIFE_KERNEL_BYTE : !strcmp(k, "bit") ? LIFE_KERNEL_BIT : -1;
@@ -302,8 +314,8 @@ int main(int argc, char **argv) {
         printf("Usage: %s input file.\n", argv[0]); /* life_cart.c:53-56 */
         return 0;
     }
-    if (kernel < 0 || gpus < 1 || bits < 0) {
-        fprintf(stderr, "life_mi355x: bad --kernel/--gpus/--format\n");
+    if (kernel < 0 || gpus < 1 || bits < 0 || partition < 0) {
+        fprintf(stderr, "life_mi355x: bad --kernel/--gpus/--format/--partition\n");
         return 1;
     }
 
@@ -328,7 +340,9 @@ int main(int argc, char **argv) {
     }
 
     life_dev *d = NULL;
-    int rc = life_dev_create(c.nx, c.ny, gpus, kernel, &d);
+    int dims[2];
+    int rc = life_dims_choose(c.nx, c.ny, gpus, partition, dims);
+    if (rc == LIFE_OK) rc = life_dev_create_ex(c.nx, c.ny, gpus, dims[0], dims[1], kernel, LIFE_XPORT_AUTO, &d);
     if (rc) die("create", rc);
     uint8_t *grid = NULL; /* dense cells: bits frames */
     char *body = NULL;    /* VTK cell text */

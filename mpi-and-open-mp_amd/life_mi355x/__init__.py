@@ -46,7 +46,7 @@ TEMPORAL_ROWS = {"bit": 48, "byte": 32}  # default register rows per wave of the
 
 # Every symbol include/life_mi355x.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = (
-    "life_decomposition", "life_dims_create", "life_halo_plan", "life_layout_query",
+    "life_decomposition", "life_dims_create", "life_dims_choose", "life_halo_plan", "life_layout_query",
     "life_strerror", "life_last_error", "life_dev_create", "life_dev_create_ex",
     "life_get_unique_id", "life_dev_create_rank", "life_dev_upload", "life_dev_fill_random",
     "life_dev_step", "life_dev_gather", "life_dev_live_count", "life_dev_sync",
@@ -97,6 +97,7 @@ def _lib():
         L.life_decomposition.restype = None
         L.life_dims_create.argtypes = [i32, P(ctypes.c_int)]
         L.life_dims_create.restype = None
+        L.life_dims_choose.argtypes = [i64, i64, i32, i32, P(ctypes.c_int)]
         L.life_halo_plan.argtypes = [i64, i64, i32, i32, i32, i32, P(HaloOp), i32]
         L.life_layout_query.argtypes = [i64, i64, i32, i32, i32, i32, P(Layout)]
         L.life_strerror.argtypes = [i32]
@@ -153,6 +154,18 @@ def dims_create(n: int):
     """MPI_Dims_create(n, 2, {0,0}) (life_cart.c:117-118)."""
     d = (ctypes.c_int * 2)()
     _lib().life_dims_create(n, d)
+    return d[0], d[1]
+
+
+PARTITIONS = {"cart": 0, "rows": 1, "cols": 2, "auto": 3}  # LIFE_PARTITION_*
+
+
+def dims_choose(nx: int, ny: int, n: int, policy="auto"):
+    """Partition shape for n shards (life_dims_choose): "cart" =
+    MPI_Dims_create, "rows" = {1, n} strips, "cols" = {n, 1}, "auto"."""
+    d = (ctypes.c_int * 2)()
+    pol = PARTITIONS[policy] if isinstance(policy, str) else int(policy)
+    _check(_lib().life_dims_choose(nx, ny, n, pol, d), "life_dims_choose")
     return d[0], d[1]
 
 

@@ -124,3 +124,32 @@ def test_plan_over_gloo(oracle, lm, kernel, world, nx, ny, gens):
         assert p.exitcode == 0
     want = oracle.life_run(oracle.fill_random(nx, ny, 42 + world, 0.45), gens)
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("kernel,world,nx,ny,gens", [
+    ("bit", 2, 96, 64, 40), ("bit", 4, 64, 4 * 33, 33), ("bit", 8, 64, 8 * 40, 37),
+    ("byte", 2, 64, 70, 35), ("byte", 4, 40, 16, 5), ("byte", 8, 64, 8 * 32, 34),
+])
+def test_row_strips_over_gloo(oracle, lm, kernel, world, nx, ny, gens):
+    """The 1-D row-strip partition (life_dims_choose "rows", dims {1, world}):
+    every message is a run of whole padded rows, up and down the ring, as in
+    5-gather/life_mpi.c:181-191 but K rows deep for the temporal layouts."""
+    dims = lm.dims_choose(nx, ny, world, "rows")
+    assert dims == (1, world)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, nx, ny, dims, gens, 7 + world, kernel, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = np.full((ny, nx), 255, np.uint8)
+    for _ in range(world):
+        rank, x0, y0, block = q.get(timeout=120)
+        assert x0 != "error", f"rank {rank}: {y0}"
+        got[y0:y0 + block.shape[0], x0:x0 + block.shape[1]] = block
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = oracle.life_run(oracle.fill_random(nx, ny, 7 + world, 0.45), gens)
+    np.testing.assert_array_equal(got, want)

@@ -71,7 +71,8 @@ def test_random_vs_reference_life_step(gpu, kernel, case):
             assert life.live_count() == case["gens"][gens][1]
 
 
-@pytest.mark.parametrize("args", [[], ["--gpus", "4"], ["--kernel", "byte"]])
+@pytest.mark.parametrize("args", [[], ["--gpus", "4"], ["--kernel", "byte"], ["--gpus", "4", "--partition", "rows"],
+                                  ["--gpus", "2", "--partition", "cols", "--kernel", "byte"]])
 def test_driver_glider_frames(gpu, tmp_path, args):
     """configs[0]: `prog glider_10x10.cfg` writes vtk/life_%06d.vtk files
     byte-identical to the reference's and prints one "%f\\n" line."""

@@ -43,6 +43,7 @@ def test_fill_random_matches_oracle(gpu, oracle, kernel, nx, ny, seed):
     (2, (0, 0), 100, 40), (4, (0, 0), 65, 33), (8, (0, 0), 300, 130), (6, (0, 0), 47, 29),
     (4, (1, 4), 70, 50), (4, (4, 1), 70, 50), (3, (3, 1), 5, 9), (2, (1, 2), 3, 2),
     (8, (4, 2), 4, 2), (4, (2, 2), 260, 260),
+    (8, (1, 8), 64, 320), (4, (1, 4), 96, 132), (2, (1, 2), 300, 70),  # row strips (temporal)
 ])
 def test_multi_shard_local(gpu, oracle, kernel, shards, dims, nx, ny):
     """P logical shards on one GPU, halo through the LOCAL transport: the same

@@ -83,6 +83,26 @@ def test_dims_create_matches_mpi(lm):
         assert lm.dims_create(n) == d
 
 
+
+def test_dims_choose_policies(lm):
+    """life_dims_choose: cart = MPI_Dims_create, rows = {1,n}, cols = {n,1},
+    auto = row strips once every strip is >= LIFE_AUTO_MIN_STRIP_ROWS tall."""
+    for n in (1, 2, 3, 4, 6, 8):
+        assert lm.dims_choose(4096, 4096, n, "cart") == lm.dims_create(n)
+        assert lm.dims_choose(4096, 4096, n, "rows") == (1, n)
+        assert lm.dims_choose(4096, 4096, n, "cols") == (n, 1)
+    assert lm.dims_choose(65536, 65536 * 8, 8, "auto") == (1, 8)  # bench weak scaling
+    assert lm.dims_choose(65536, 65536, 8, "auto") == (1, 8)      # strong: 8192-row strips
+    assert lm.dims_choose(10, 10, 4, "auto") == (2, 2)            # glider: strips too short
+    assert lm.dims_choose(500, 500, 8, "auto") == (4, 2)
+    assert lm.dims_choose(8192, 8191, 8, "auto") == (4, 2)        # 1023-row strips
+    with pytest.raises(lm.LifeError):
+        lm.dims_choose(10, 3, 4, "rows")  # empty strips
+    with pytest.raises(lm.LifeError):
+        lm.dims_choose(10, 10, 0, "cart")
+    with pytest.raises(lm.LifeError):
+        lm.dims_choose(10, 10, 2, 7)
+
 @pytest.mark.parametrize("kernel", ["byte", "bit"])
 @pytest.mark.parametrize("nx,ny,dims", [(1, 1, (1, 1)), (65536, 65536, (1, 1)), (1000, 37, (4, 2)),
                                         (3, 2, (3, 2)), (262144, 131072, (4, 2))])
