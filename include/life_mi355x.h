@@ -207,8 +207,9 @@ int life_dev_world(life_dev *d, int *world, int *dims0, int *dims1, int *nlocal,
 int life_dev_set_timing(life_dev *d, int on);
 
 /* Execution-path switches (defaults 1): LIFE_OPT_SMALL_GRID lets a
- * single-shard grid that fits one CU's LDS run all generations of a step call
- * in one resident-workgroup launch; LIFE_OPT_OVERLAP overlaps the halo
+ * single-shard grid that fits one CU run all generations of a step call in
+ * one resident-workgroup launch (1: the grid in VGPRs when its shape allows,
+ * else in LDS; 2: LDS only; 0: off); LIFE_OPT_OVERLAP overlaps the halo
  * exchange with the interior kernel on partitioned grids.  Results are
  * identical either way (tests switch them to reach every kernel). */
 #define LIFE_OPT_SMALL_GRID 1

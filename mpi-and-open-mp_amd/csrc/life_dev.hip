@@ -100,7 +100,7 @@ struct life_dev {
     bool rank_mode = false;
     bool timing = false;
     bool overlap = true;
-    bool small_ok = true;  // LDS-resident path for grids that fit one CU
+    int small_mode = 1;  // grids that fit one CU: 0 off, 1 VGPR kernel else LDS kernel, 2 LDS kernel
     std::vector<Shard> shards;
     double acc_ms = 0.0;
     int64_t acc_launches = 0;
@@ -687,8 +687,9 @@ int life_dev_fill_random(life_dev *d, uint64_t seed, uint32_t thr32) {
 // A single-shard grid small enough for one CU's LDS runs every generation of
 // the call in one resident-workgroup launch (life_kernels.hip, small_kernel).
 static bool small_grid(const life_dev *d) {
-    return d->world == 1 && d->shards.size() == 1 && d->small_ok &&
-           life::small_lds_bytes(d->shards[0].lay) <= life::kSmallMaxLds;
+    if (d->world != 1 || d->shards.size() != 1 || d->small_mode == 0) return false;
+    const life_layout &L = d->shards[0].lay;
+    return (d->small_mode == 1 && life::reg_small_rows(L) > 0) || life::small_lds_bytes(L) <= life::kSmallMaxLds;
 }
 
 static int step_small(life_dev *d, int64_t generations) {
@@ -701,7 +702,10 @@ static int step_small(life_dev *d, int64_t generations) {
         if (!t) return rc;
         HIPCHK(hipEventRecord(t->a, s.stream));
     }
-    HIPCHK(life::launch_small(s.lay, s.buf[s.cur], s.buf[s.cur ^ 1], generations, s.stream));
+    if (d->small_mode == 1 && life::reg_small_rows(s.lay) > 0)
+        HIPCHK(life::launch_reg_small(s.lay, s.buf[s.cur], s.buf[s.cur ^ 1], generations, s.stream));
+    else
+        HIPCHK(life::launch_small(s.lay, s.buf[s.cur], s.buf[s.cur ^ 1], generations, s.stream));
     if (t) {
         HIPCHK(hipEventRecord(t->b, s.stream));
         // LDS-resident: HBM sees one import and one export of the grid per launch
@@ -905,7 +909,10 @@ int life_dev_configure(life_dev *d, int option, int value) {
     if (!d) return LIFE_EINVAL;
     CHK(life_dev_sync(d));
     switch (option) {
-    case LIFE_OPT_SMALL_GRID: d->small_ok = value != 0; return LIFE_OK;
+    case LIFE_OPT_SMALL_GRID:
+        if (value < 0 || value > 2) return LIFE_EINVAL;
+        d->small_mode = value;
+        return LIFE_OK;
     case LIFE_OPT_OVERLAP: d->overlap = value != 0; return LIFE_OK;
     default: return LIFE_EINVAL;
     }

@@ -76,6 +76,13 @@ void set_temporal_rows(int kernel, int nr);  // kernel -1: both encodings
 constexpr int64_t kSmallMaxLds = 160 * 1024;
 int64_t small_lds_bytes(const life_layout &L);
 hipError_t launch_small(const life_layout &L, const uint8_t *in, uint8_t *out, int64_t gens, hipStream_t s);
+// Register-resident variant (one 1024-lane workgroup, the grid in VGPRs):
+// usable when reg_small_rows(L) > 0 (at most 64 words per row and a strip
+// height R from its instance list dividing h with h/R strips fitting the
+// workgroup's lane groups); in != out.
+int reg_small_rows(const life_layout &L);
+hipError_t launch_reg_small(const life_layout &L, const uint8_t *in, uint8_t *out, int64_t gens,
+                            hipStream_t s);
 
 // Column halo staging: pack writes the last xapron columns to slot 0 and the
 // first xapron columns to slot 1 (h rows each: 1 byte 0/1 per row for a cell

@@ -639,6 +639,129 @@ __global__ __launch_bounds__(kSmallThreads) void small_kernel(SArgs a) {
     }
 }
 
+// ------------------------------------------------------- small grids, in VGPRs
+// Register-resident variant of the small-grid path (configs[1] p46gun_big
+// 500^2).  One 1024-lane workgroup holds the whole grid in VGPRs: a wave is
+// split into 64/Wp lane groups (Wp = W rounded up to a power of two), each
+// group owns a strip of R consecutive rows, one word column per lane; the
+// grid is ns = h/R strips (R divides h, so every strip is full).  Per
+// generation a lane computes the 2-bit horizontal sums of its R rows
+// (neighbour words by ds_bpermute inside the group, periodic in x),
+// publishes the sums of its first and last row in LDS, one barrier, reads the
+// strip above's last / the strip below's first sums (periodic in y), and
+// applies the rule to its R rows.  PATCH (w % 32 != 0): the x wrap crosses a
+// partial word, so cell w-1 is moved to bit 31 of word 0's left word and
+// cell 0 is put at bit q of the last word before the sums.
+constexpr int kRegThreads = 1024;
+constexpr int kRegMaxW = 64;
+
+struct RArgs {
+    const uint8_t *in;
+    uint8_t *out;
+    int64_t pitch, xoff, ya;
+    int32_t w, h, W, lgWp, gens, bit, ns;
+};
+
+template <int R, bool PATCH>
+__global__ __launch_bounds__(kRegThreads) void rsmall_kernel(RArgs a) {
+    __shared__ uint32_t xch[2][4][kRegThreads];  // [parity][top s0/s1, bottom s0/s1][thread]
+    const int t = threadIdx.x;
+    const int Wp = 1 << a.lgWp, W = a.W;
+    const int j = t & (Wp - 1);  // word column
+    const int st = t >> a.lgWp;  // strip
+    const bool active = st < a.ns && j < W;
+    const int base = (t & 63) & ~(Wp - 1);  // first lane of this lane group
+    const int jl = j == 0 ? W - 1 : j - 1, jr = j + 1 >= W ? 0 : j + 1;
+    const int addr_l = (base + jl) << 2, addr_r = (base + jr) << 2;
+    const int q = a.w - 32 * (W - 1);  // valid cells in the last word: 1..32
+    const bool last = j == W - 1;
+    const uint32_t keep = (last && q < 32) ? (1u << q) - 1u : 0xFFFFFFFFu;
+    const uint32_t lsh = j == 0 ? (uint32_t)((32 - q) & 31) : 0u;  // cell w-1 -> bit 31
+    const uint32_t qs = (uint32_t)(q & 31);
+    const int sa = st == 0 ? a.ns - 1 : st - 1, sb = st + 1 >= a.ns ? 0 : st + 1;
+    const int ta = ((sa << a.lgWp) + j) & (kRegThreads - 1), tb = ((sb << a.lgWp) + j) & (kRegThreads - 1);
+    const int y0 = st * R;
+
+    uint32_t v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        uint32_t x = 0;
+        if (active) {
+            const uint8_t *row = a.in + (int64_t)(y0 + r + a.ya) * a.pitch + a.xoff;
+            if (a.bit) {
+                x = reinterpret_cast<const uint32_t *>(row)[j];
+            } else {
+                for (int k = 0; k < 32 && 32 * j + k < a.w; ++k) x |= (uint32_t)(row[32 * j + k] != 0) << k;
+            }
+        }
+        v[r] = x;
+    }
+    auto hsum = [&](uint32_t c, uint32_t &s0, uint32_t &s1) {
+        uint32_t l = bperm(addr_l, c);
+        const uint32_t rw = bperm(addr_r, c);
+        if (PATCH) {
+            l <<= lsh;
+            // (c & keep) | (rw << qs & ~keep): the last word gets cell 0 at bit q (above it: don't-care)
+            c = b3<((0xF0 & 0xCC) | (~0xCC & 0xAA)) & 0xFF>(c, keep, rw << qs);
+        }
+        BitEnc::fa(__builtin_amdgcn_alignbit(c, l, 31), c, __builtin_amdgcn_alignbit(rw, c, 1), s0, s1);
+    };
+    for (int g = 0; g < a.gens; ++g) {
+        const int par = g & 1;
+        uint32_t h0[R], h1[R];
+        hsum(v[0], h0[0], h1[0]);
+        if (R > 1) hsum(v[R - 1], h0[R - 1], h1[R - 1]);
+        xch[par][0][t] = h0[0];
+        xch[par][1][t] = h1[0];
+        xch[par][2][t] = h0[R - 1];
+        xch[par][3][t] = h1[R - 1];
+        __syncthreads();
+        const uint32_t a0 = xch[par][2][ta], a1 = xch[par][3][ta];
+        const uint32_t d0 = xch[par][0][tb], d1 = xch[par][1][tb];
+#pragma unroll
+        for (int r = 1; r < R - 1; ++r) hsum(v[r], h0[r], h1[r]);
+#pragma unroll
+        for (int r = 1; r < R - 1; ++r)
+            v[r] = BitEnc::rule1(h0[r - 1], h1[r - 1], h0[r], h1[r], h0[r + 1], h1[r + 1], v[r]);
+        if (R == 1) {
+            v[0] = BitEnc::rule1(a0, a1, h0[0], h1[0], d0, d1, v[0]);
+        } else {
+            v[0] = BitEnc::rule1(a0, a1, h0[0], h1[0], h0[1], h1[1], v[0]);
+            v[R - 1] = BitEnc::rule1(h0[R - 2], h1[R - 2], h0[R - 1], h1[R - 1], d0, d1, v[R - 1]);
+        }
+    }
+    if (!active) return;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        uint8_t *row = a.out + (int64_t)(y0 + r + a.ya) * a.pitch + a.xoff;
+        const uint32_t x = v[r] & keep;
+        if (a.bit) {
+            reinterpret_cast<uint32_t *>(row)[j] = x;
+        } else {
+            for (int k = 0; k < 32 && 32 * j + k < a.w; ++k) row[32 * j + k] = (uint8_t)((x >> k) & 1u);
+        }
+    }
+}
+
+// Strip heights with a kernel instance: the smallest that divides h and
+// gives at most kRegThreads / Wp strips is used.
+constexpr int kRegRows[] = {1, 2, 3, 4, 5, 6, 8, 10, 12, 16, 20, 25, 32};
+
+template <bool PATCH>
+hipError_t launch_rs(const RArgs &a, int R, hipStream_t s) {
+    // only the waves that own strips (the barrier counts the launched waves)
+    const unsigned threads = (unsigned)((((int64_t)a.ns << a.lgWp) + 63) / 64 * 64);
+    switch (R) {
+#define LIFE_RS(N) \
+    case N: rsmall_kernel<N, PATCH><<<1, threads, 0, s>>>(a); break;
+        LIFE_RS(1) LIFE_RS(2) LIFE_RS(3) LIFE_RS(4) LIFE_RS(5) LIFE_RS(6) LIFE_RS(8) LIFE_RS(10) LIFE_RS(12)
+        LIFE_RS(16) LIFE_RS(20) LIFE_RS(25) LIFE_RS(32)
+#undef LIFE_RS
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ cell access
 // Byte: cell x of a padded row at row[xoff + x].  Bit: word (x >> 5) (floor)
 // of the dword array starting at row + xoff, bit (x & 31).
@@ -1092,6 +1215,38 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
                        : K == 24 ? launch_k<false, 24>(a, wrap, grid, s) : launch_k<false, 32>(a, wrap, grid, s);
     return K == 16 ? launch_k<true, 16>(a, wrap, grid, s)
                    : K == 24 ? launch_k<true, 24>(a, wrap, grid, s) : launch_k<true, 32>(a, wrap, grid, s);
+}
+
+int reg_small_rows(const life_layout &L) {
+    const int64_t W = (L.w + 31) / 32;
+    if (W > kRegMaxW || L.h <= 0) return 0;
+    int64_t Wp = 1;
+    while (Wp < W) Wp <<= 1;
+    const int64_t strips = kRegThreads / Wp;
+    for (int R : kRegRows)
+        if (L.h % R == 0 && L.h / R <= strips) return R;
+    return 0;
+}
+
+hipError_t launch_reg_small(const life_layout &L, const uint8_t *in, uint8_t *out, int64_t gens,
+                            hipStream_t s) {
+    const int R = reg_small_rows(L);
+    if (R == 0 || gens <= 0 || gens > INT32_MAX) return hipErrorInvalidValue;
+    RArgs a;
+    a.in = in;
+    a.out = out;
+    a.pitch = L.pitch;
+    a.xoff = L.xoff;
+    a.ya = L.yapron;
+    a.w = (int32_t)L.w;
+    a.h = (int32_t)L.h;
+    a.W = (int32_t)((L.w + 31) / 32);
+    a.lgWp = 0;
+    while ((1 << a.lgWp) < a.W) ++a.lgWp;
+    a.gens = (int32_t)gens;
+    a.bit = is_bit(L) ? 1 : 0;
+    a.ns = (int32_t)(L.h / R);
+    return L.w % 32 ? launch_rs<true>(a, R, s) : launch_rs<false>(a, R, s);
 }
 
 int64_t small_lds_bytes(const life_layout &L) {

@@ -225,8 +225,11 @@ class Life:
         else:
             _check(_lib().life_dev_create_ex(self.nx, self.ny, shards, dims[0], dims[1], self.kernel,
                                              transport, ctypes.byref(self._h)), "life_dev_create")
-        if not small_grid:
-            self.configure(OPT_SMALL_GRID, 0)
+        # small_grid: True/"auto" (VGPR kernel when the shape allows, else LDS),
+        # "lds" (LDS kernel only), False (the streaming kernels)
+        mode = {True: 1, "auto": 1, "lds": 2, False: 0}[small_grid]
+        if mode != 1:
+            self.configure(OPT_SMALL_GRID, mode)
         if not overlap:
             self.configure(OPT_OVERLAP, 0)
 

@@ -1,5 +1,5 @@
-"""configs[1] (p46gun_big 500^2, 10 000 generations): LDS-resident small
-kernel vs the temporally blocked HBM kernel at several tile heights, one
+"""configs[1] (p46gun_big 500^2, 10 000 generations): VGPR- and LDS-resident
+small-grid kernels vs the temporally blocked HBM kernel at several tile heights, one
 process (the LIFE_TEMPORAL_DEPTH env picks K).  Prints one JSON line per mode."""
 import json
 import os
@@ -13,12 +13,13 @@ import life_mi355x as lm  # noqa: E402
 _, _, grid = lm.load_cfg(os.path.join(ROOT, "tests", "golden", "cfg", "p46gun_big.cfg"))
 ny, nx = grid.shape
 GENS = 10000
-modes = [("small", 0)] + [("tstep", r) for r in (32, 40, 48, 56, 64, 96)]
+modes = [("vgpr", 0), ("lds", 0)] + [("tstep", r) for r in (32, 48)]
 for rnd in range(2):
     for name, rows in modes:
         if rows:
             lm.tune_temporal(rows, "bit")
-        with lm.Life(nx, ny, kernel="bit", small_grid=(name == "small")) as life:
+        small = {"vgpr": True, "lds": "lds", "tstep": False}[name]
+        with lm.Life(nx, ny, kernel="bit", small_grid=small) as life:
             life.upload(grid)
             life.step(64)
             life.sync()

@@ -12,12 +12,13 @@ SIZES = [(1, 1), (1, 5), (5, 1), (2, 3), (3, 2), (16, 16), (17, 3), (31, 33), (6
          (65, 65), (127, 5), (128, 128), (129, 130), (200, 1), (1000, 37), (257, 300)]
 
 
-@pytest.mark.parametrize("small", [False, True], ids=["stream", "lds"])
+@pytest.mark.parametrize("small", [False, "lds", True], ids=["stream", "lds", "vgpr"])
 @pytest.mark.parametrize("kernel", ["byte", "bit"])
 @pytest.mark.parametrize("nx,ny", SIZES)
 def test_single_shard(gpu, oracle, kernel, nx, ny, small):
     """stream: the HBM-streaming kernels (one-generation or temporal);
-    lds: the LDS-resident small-grid path."""
+    lds: the LDS-resident small-grid kernel; vgpr: the register-resident one
+    where the shape allows it (else LDS)."""
     g0 = oracle.fill_random(nx, ny, seed=nx * 1000 + ny, density=0.4)
     with gpu.Life(nx, ny, shards=1, kernel=kernel, small_grid=small) as life:
         life.upload(g0)
@@ -165,13 +166,18 @@ def test_temporal_tile_heights_agree(gpu, oracle, kernel, rows):
         gpu.tune_temporal(gpu.TEMPORAL_ROWS[kernel], kernel)
 
 
-# ---------------------------------------------------------------- LDS-resident small grids
+# ---------------------------------------------------------------- CU-resident small grids
+@pytest.mark.parametrize("small", ["lds", True], ids=["lds", "vgpr"])
 @pytest.mark.parametrize("kernel", ["bit", "byte"])
 @pytest.mark.parametrize("nx,ny,gens", [(500, 500, 300), (1, 1, 5), (33, 2, 17), (31, 31, 40), (1000, 600, 50),
-                                        (32768, 19, 9), (64, 3, 100), (97, 1, 12)])
-def test_small_grid_path(gpu, oracle, kernel, nx, ny, gens):
+                                        (32768, 19, 9), (64, 3, 100), (97, 1, 12),
+                                        # VGPR kernel shapes: strip heights 1..32, 1..64 words per row
+                                        (300, 100, 77), (10, 10, 33), (2048, 512, 21), (2047, 480, 19),
+                                        (64, 1000, 45), (100, 96, 60), (1, 7, 9), (40, 20, 100),
+                                        (1984, 400, 25), (96, 125, 64)])
+def test_small_grid_path(gpu, oracle, kernel, nx, ny, gens, small):
     g0 = oracle.fill_random(nx, ny, seed=nx ^ ny, density=0.4)
-    with gpu.Life(nx, ny, kernel=kernel) as life:
+    with gpu.Life(nx, ny, kernel=kernel, small_grid=small) as life:
         life.upload(g0)
         life.step(gens)
         np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, gens, threads=4))
