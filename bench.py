@@ -179,6 +179,10 @@ def main():
     updates_per_launch, valu_per_launch = life.kernel_work()
     live = life.live_count()
 
+    # a measured stream-copy ceiling next to the spec peak
+    # (rank 0's GPU, after the timed region; 2 x 2 GiB buffers)
+    copy_gbps = lm.measure_copy(local_rank, 2 << 30, 5) if rank == 0 else 0.0
+
     if rank == 0:
         cells = float(nx) * float(ny) * a.steps
         bpu = 0.25 if a.kernel == "bit" else 2.0  # algorithmic HBM bytes per cell-update
@@ -220,6 +224,8 @@ def main():
                          # the north-star question "% of HBM roofline" in cell-update terms: the
                          # rate a one-generation-per-HBM-pass kernel would reach at the HBM peak on
                          # n_gpus GPUs (8 TB/s / 0.25 B or 2 B per update), and value against it
+                         "copy_ceiling_GBps": round(copy_gbps, 1),
+                         "frac_of_copy_ceiling": round(achieved / copy_gbps, 4) if copy_gbps > 0 else None,
                          "hbm_bound_cell_rate": round(n_gpus * HBM_PEAK_GBS / bpu, 1),
                          "cell_rate_vs_hbm_bound": round(value / (n_gpus * HBM_PEAK_GBS / bpu), 4)},
         }

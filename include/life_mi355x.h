@@ -237,6 +237,12 @@ int life_tune(int kernel, int rows, int depth);
  * LIFE_TEMPORAL_ROWS / LIFE_TEMPORAL_ROWS_BYTE override at load time. */
 int life_tune_temporal(int kernel, int rows);
 
+/* Measured HBM copy ceiling of `device` ("also report a
+ * measured stream-copy ceiling"): a 16-B-per-lane grid-stride copy kernel over
+ * two fresh `bytes`-sized buffers, best of `reps` runs timed with HIP events;
+ * *gbps = 2 * bytes (read + write) / time.  Allocates and frees its buffers. */
+int life_measure_copy(int device, int64_t bytes, int reps, double *gbps);
+
 /* life_free (life_cart.c:146-157). */
 void life_dev_destroy(life_dev *d);
 

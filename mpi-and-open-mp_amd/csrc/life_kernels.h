@@ -122,4 +122,7 @@ hipError_t launch_fill_random(const life_layout &L, int64_t nx, uint64_t key, ui
 hipError_t launch_census(const life_layout &L, int64_t nx, const uint8_t *buf, unsigned long long *out,
                          hipStream_t s);
 
+// Copy-ceiling probe: out[0, bytes) = in[0, bytes), bytes a multiple of 16.
+hipError_t launch_copy(const void *in, void *out, int64_t bytes, hipStream_t s);
+
 }  // namespace life

@@ -1336,6 +1336,25 @@ hipError_t launch_vtk_block(const life_layout &L, const uint8_t *buf, uint8_t *o
     return hipGetLastError();
 }
 
+namespace {
+// Copy ceiling: one 16-B load + store per lane, one wave-instruction each,
+// a workgroup per 4 KiB.  Measured against grid-stride, unrolled and
+// nontemporal variants (scripts/ubench_copy.hip, profiles/r01/ubench_copy.txt):
+// this shape is the fastest, 6.30 TB/s on 2 GiB.
+__global__ __launch_bounds__(256) void copy_kernel(const uint4 *__restrict__ in, uint4 *__restrict__ out,
+                                                   int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) out[i] = in[i];
+}
+}  // namespace
+
+hipError_t launch_copy(const void *in, void *out, int64_t bytes, hipStream_t s) {
+    const int64_t n = bytes / 16;
+    copy_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(reinterpret_cast<const uint4 *>(in),
+                                                            reinterpret_cast<uint4 *>(out), n);
+    return hipGetLastError();
+}
+
 hipError_t launch_census(const life_layout &L, int64_t nx, const uint8_t *buf, unsigned long long *out,
                          hipStream_t s) {
     const dim3 grid(blocks_for(L.units, 256), (unsigned)(L.h < 4096 ? L.h : 4096));

@@ -52,7 +52,7 @@ ABI_SYMBOLS = (
     "life_dev_step", "life_dev_gather", "life_dev_live_count", "life_dev_sync",
     "life_dev_layout", "life_dev_world", "life_dev_set_timing", "life_dev_kernel_stats",
     "life_tune", "life_tune_temporal", "life_dev_configure", "life_dev_kernel_work", "life_dev_checksum",
-    "life_dev_gather_vtk", "life_dev_destroy",
+    "life_dev_gather_vtk", "life_dev_destroy", "life_measure_copy",
 )
 
 
@@ -124,6 +124,7 @@ def _lib():
         L.life_dev_kernel_work.argtypes = [vp, P(ctypes.c_double), P(ctypes.c_double)]
         L.life_tune.argtypes = [i32, i32, i32]
         L.life_tune_temporal.argtypes = [i32, i32]
+        L.life_measure_copy.argtypes = [i32, i64, i32, P(ctypes.c_double)]
         L.life_dev_destroy.argtypes = [vp]
         L.life_dev_destroy.restype = None
         _LIB = L
@@ -197,6 +198,13 @@ def tune_temporal(rows: int = 0, kernel=-1) -> None:
 def tune(rows: int = 0, depth: int = 0, kernel=-1) -> None:
     """Stencil rows-per-lane / prefetch depth for this process (life_tune)."""
     _check(_lib().life_tune(kernel_id(kernel), rows, depth), "life_tune")
+
+
+def measure_copy(device: int = 0, nbytes: int = 2 << 30, reps: int = 5) -> float:
+    """Measured HBM copy ceiling in GB/s (read + write bytes / best time)."""
+    g = ctypes.c_double()
+    _check(_lib().life_measure_copy(device, nbytes, reps, ctypes.byref(g)), "life_measure_copy")
+    return g.value
 
 
 def unique_id() -> bytes:

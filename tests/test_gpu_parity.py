@@ -212,3 +212,10 @@ def test_step_right_after_async_fill(gpu, oracle, kernel):
         got = life.checksum()
     want = oracle.life_run(oracle.fill_random(nx, ny, 9, 0.5), gens, threads=8)
     assert got == oracle.checksum(want)
+
+
+def test_measure_copy_ceiling(gpu):
+    """life_measure_copy (bench's live copy ceiling): a plausible HBM rate
+    (MI355X spec 8 TB/s; ~6.3 TB/s measured for a float4 copy)."""
+    g = gpu.measure_copy(0, 1 << 30, 3)
+    assert 2000.0 < g < 8000.0, g
