@@ -214,6 +214,17 @@ int life_dev_set_timing(life_dev *d, int on);
  * identical either way (tests switch them to reach every kernel). */
 #define LIFE_OPT_SMALL_GRID 1
 #define LIFE_OPT_OVERLAP 2
+/* LIFE_OPT_CHAIN (default 0): temporal layouts run chained tiles -- one
+ * workgroup walks a segment of a tile column, each K-generation window fed
+ * the exact row above it by the previous window (life_kernels.hip
+ * tchain_kernel); 0: independent tiles (tstep_kernel); a value v > 1 also
+ * sizes every chained launch to about v workgroups (default: 2 per CU), which
+ * makes small grids walk long chains (tests).  Bit-exact, but measured
+ * slower than independent tiles at 65536^2 (bit 0-10 %, byte 20-25 %,
+ * profiles/r01/chain_sweep.jsonl): every chain starts together and walks its
+ * windows in lockstep, so the whole chip loads, then computes, and the load
+ * phase the independent tiles hide is exposed. */
+#define LIFE_OPT_CHAIN 3
 int life_dev_configure(life_dev *d, int option, int value);
 int life_dev_kernel_stats(life_dev *d, double *avg_ms, int64_t *launches, double *bytes_per_launch);
 /* The same timed launches: mean cell-updates per launch (cells x generations

@@ -100,6 +100,8 @@ struct life_dev {
     bool rank_mode = false;
     bool timing = false;
     bool overlap = true;
+    bool chain = false;   // chained temporal tiles where supported (LIFE_OPT_CHAIN; measured slower, off)
+    int chain_slots = 0;  // > 0: workgroups per chained launch (tests: long chains on small grids)
     int small_mode = 1;  // grids that fit one CU: 0 off, 1 VGPR kernel else LDS kernel, 2 LDS kernel
     std::vector<Shard> shards;
     double acc_ms = 0.0;
@@ -396,6 +398,36 @@ int launch_tiles(life_dev *d, Shard &s, const life::TileRegion *r, int nreg, int
     return LIFE_OK;
 }
 
+// Chained temporal tiles over tile columns [tx0, tx1) x owned rows [yb, ye)
+// (life::launch_tchain), with the same timing bookkeeping as launch_tiles.
+int launch_chain(life_dev *d, Shard &s, int64_t tx0, int64_t tx1, int64_t yb, int64_t ye, int m, int reserve,
+                 bool timed, hipStream_t st) {
+    const uint8_t *in = s.buf[s.cur];
+    uint8_t *out = s.buf[s.cur ^ 1];
+    TimedLaunch *t = nullptr;
+    if (d->timing && timed) {
+        int rc;
+        t = timer_slot(s, &rc);
+        if (!t) return rc;
+        HIPCHK(hipEventRecord(t->a, st));
+    }
+    double windows = 0.0;
+    const int slots = d->chain_slots > 0 ? d->chain_slots : life::chain_slots(s.lay, reserve);
+    HIPCHK(life::launch_tchain(s.lay, in, out, tx0, tx1, yb, ye, m, wrap_of(d), slots, st, &windows));
+    if (t) {
+        HIPCHK(hipEventRecord(t->b, st));
+        const life::TileGeom g = life::tile_geom(s.lay);
+        const int64_t xa = tx0 * g.words * 32, xb = std::min(tx1 * g.words * 32, s.lay.w);
+        const double cells = (double)(xb - xa) * (double)(std::min(ye, s.lay.h) - yb);
+        d->acc_bytes += cells * (s.lay.kernel == LIFE_KERNEL_BIT ? 0.25 : 2.0);
+        d->acc_updates += cells * (double)m;
+        d->acc_valu += windows * 64.0 * life::tstep_valu_per_tile_lane(m, s.lay.kernel == LIFE_KERNEL_BYTE);
+    }
+    return LIFE_OK;
+}
+
+bool use_chain(const life_dev *d, const Shard &s) { return d->chain && life::chain_supported(s.lay); }
+
 // Block boundary of the overlapped schedule: both compute streams wait for
 // the interior (stream2), the ring (stream) and the halo (comm stream).
 int join_streams(Shard &s) {
@@ -422,8 +454,12 @@ int generation_block(life_dev *d, int m) {
         for (Shard &s : d->shards) {
             HIPCHK(hipSetDevice(s.device));
             const life::TileGeom g = life::tile_geom(s.lay);
-            const life::TileRegion all{0, g.ntx, 0, g.nty};
-            CHK(launch_tiles(d, s, &all, 1, m, true, s.stream));
+            if (use_chain(d, s)) {
+                CHK(launch_chain(d, s, 0, g.ntx, 0, s.lay.h, m, 0, true, s.stream));
+            } else {
+                const life::TileRegion all{0, g.ntx, 0, g.nty};
+                CHK(launch_tiles(d, s, &all, 1, m, true, s.stream));
+            }
         }
         for (Shard &s : d->shards) s.cur ^= 1;
         return LIFE_OK;
@@ -454,7 +490,17 @@ int generation_block(life_dev *d, int m) {
         HIPCHK(hipEventRecord(s.ev_ring, s.stream));
         HIPCHK(hipStreamWaitEvent(s.comm_stream, s.ev_ring, 0));
         const life::TileRegion inner{ca, cb, ra, rb};
-        if (rb > ra && cb > ca) CHK(launch_tiles(d, s, &inner, 1, m, true, s.stream2));
+        if (rb > ra && cb > ca) {
+            if (use_chain(d, s)) {
+                // leave the slots of the concurrent ring tiles (and a few for RCCL) free
+                int64_t ring_tiles = 0;
+                for (int k = 0; k < n; k++) ring_tiles += (ring[k].tx1 - ring[k].tx0) * (ring[k].ty1 - ring[k].ty0);
+                CHK(launch_chain(d, s, ca, cb, ra * g.rows, std::min(rb * g.rows, s.lay.h), m,
+                                 (int)std::min<int64_t>(ring_tiles + 8, 1 << 20), true, s.stream2));
+            } else {
+                CHK(launch_tiles(d, s, &inner, 1, m, true, s.stream2));
+            }
+        }
     }
     CHK(exchange(d, 1, true));
     for (Shard &s : d->shards) {
@@ -914,6 +960,11 @@ int life_dev_configure(life_dev *d, int option, int value) {
         d->small_mode = value;
         return LIFE_OK;
     case LIFE_OPT_OVERLAP: d->overlap = value != 0; return LIFE_OK;
+    case LIFE_OPT_CHAIN:
+        if (value < 0) return LIFE_EINVAL;
+        d->chain = value != 0;
+        d->chain_slots = value > 1 ? value : 0;
+        return LIFE_OK;
     default: return LIFE_EINVAL;
     }
 }

@@ -64,6 +64,17 @@ constexpr int64_t kTemporalSlackRows = 8 * 96;
 hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, const TileRegion *r, int nreg,
                         int m, Wrap wrap, hipStream_t s);
 int temporal_rows(bool bit);      // register rows per wave (32/40/48/56/64/96)
+// Chained temporal tiles (tchain_kernel): the tile columns [tx0, tx1) x owned
+// rows [yb, ye) of a temporal layout, one workgroup per segment of a tile
+// column walking K-generation windows top to bottom (each window's top row
+// fed by the one above it).  Segments are sized so the launch is about
+// `slots` workgroups (chain_slots(L, reserve): the resident workgroups per CU
+// x CUs, minus `reserve` slots left to concurrent work).  *windows = windows
+// computed (VALU model).
+bool chain_supported(const life_layout &L);  // K = 32 and the tile height has an instance
+int chain_slots(const life_layout &L, int reserve);
+hipError_t launch_tchain(const life_layout &L, const uint8_t *in, uint8_t *out, int64_t tx0, int64_t tx1,
+                         int64_t yb, int64_t ye, int m, Wrap wrap, int slots, hipStream_t s, double *windows);
 // VALU instructions the lanes at one lane position of a tile's waves issue
 // for m generations (the op-count model of life_kernels.hip tstep_kernel,
 // checked against the SQ_INSTS_VALU counter in profiles/); x 64 lanes x tiles.

@@ -544,6 +544,170 @@ __global__ __launch_bounds__(64 * kStackWaves, 4) void tstep_kernel(TArgs a) {  
     }
 }
 
+// Chained temporal tiles: one workgroup walks a SEGMENT of a tile column top
+// to bottom, one K-generation window after the other, and hands each
+// window's last exact row down to the next window through LDS.  The same 8
+// stacked waves and per-generation barrier as tstep_kernel; what changes:
+// the horizontal sums of window row 8R-K-1 (exact for every generation the
+// launch runs) are kept per generation in `hist`, and the next window, which
+// starts right below them, takes them as the row above its top row instead of
+// zeros.  Its top rows stay exact, so a fed window stores 8R-K rows instead
+// of 8R-2K (bit R = 48: 352 instead of 320 of 384 rows computed), and one
+// launch is one round of ~2 workgroups per CU (segments sized to the CU count)
+// instead of ~14 rounds of tiles with a partial last round.
+struct CArgs {
+    const uint8_t *in;
+    uint8_t *out;
+    int64_t pitch, xoff, W, h, ya;
+    int64_t tx0, ncols;     // tile columns [tx0, tx0 + ncols)
+    int64_t yb, ye, seg;    // owned rows [yb, ye) in segments of `seg` rows
+    int32_t m;
+};
+
+template <bool BYTE, int R, int K, bool WRAPX, bool WRAPY>
+__global__ __launch_bounds__(64 * kStackWaves, 6) void tchain_kernel(CArgs a) {  // 6 waves/SIMD: 3 windows per CU, as tstep_kernel reaches
+    static_assert(R >= 3 && K >= 1 && K <= 32 && kStackWaves * R - K - 1 >= 0, "window");
+    constexpr int NW = kStackWaves;
+    constexpr int HW = (NW * R - K - 1) / R, HR = (NW * R - K - 1) % R;  // the handed-down row
+    __shared__ uint32_t xch[2][NW][4][64];
+    __shared__ uint32_t hist[2][K][2][64];  // [window parity][generation][s0/s1][lane]
+    __shared__ uint32_t junk[NW][2][64];     // where the other waves' copies of that row go
+    const int lane = threadIdx.x & 63;
+    const int wi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#if LIFE_HSUM_MODE == 3
+    __shared__ uint32_t rowx[NW][66];
+    uint32_t *slot = rowx[wi];
+    if (lane < 2) slot[lane * 65] = 0u;
+#else
+    uint32_t *slot = nullptr;
+#endif
+    const int64_t tx = a.tx0 + (int64_t)blockIdx.x % a.ncols;
+    const int64_t s0 = a.yb + (int64_t)(blockIdx.x / a.ncols) * a.seg;
+    const int64_t s1 = s0 + a.seg < a.ye ? s0 + a.seg : a.ye;
+    if (s0 >= s1) return;  // whole workgroup
+    const int64_t j = tx * 62 + lane - 1;
+    int64_t jl;
+    if (WRAPX) {
+        jl = j % a.W;
+        if (jl < 0) jl += a.W;
+    } else {
+        jl = j > a.W ? a.W : j;
+    }
+    const uint32_t voff = (uint32_t)(a.xoff + (BYTE ? 32 : 4) * jl);
+    const bool st = lane >= 1 && lane <= 62 && j < a.W;
+    const uint8_t *row0 = a.in + a.ya * a.pitch;
+    int64_t top = s0 - K;  // window top (owned row of wave 0's register row 0)
+    for (int win = 0;; ++win) {
+        const bool fed = win > 0;
+        const int hp = win & 1;
+        // Every wave stores its copy of register row HR each generation (no
+        // branch inside the unrolled row loop: that split costs ~27 VGPRs);
+        // only wave HW's lands in hist.
+        uint32_t *const hdst = wi == HW ? &hist[hp ^ 1][0][0][0] : &junk[wi][0][0];
+        const int hstride = wi == HW ? 128 : 0;
+        const int64_t y0 = top + (int64_t)wi * R;
+        int64_t y = y0;
+        if (WRAPY) {
+            y %= a.h;
+            if (y < 0) y += a.h;
+        }
+        const uint8_t *p = row0 + y * a.pitch;
+        uint32_t v[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (BYTE) {
+                const uint4 *q = reinterpret_cast<const uint4 *>(p + voff);
+                v[r] = pack32(q[0], q[1]);
+            } else {
+                v[r] = *reinterpret_cast<const uint32_t *>(p + voff);
+            }
+            ++y;
+            if (WRAPY && y == a.h) {
+                y = 0;
+                p = row0;
+            } else {
+                p += a.pitch;
+            }
+        }
+        for (int g = 0; g < a.m; ++g) {
+            const int par = g & 1;
+            uint32_t t0, t1, b0, b1;
+            bit_hsum(v[0], t0, t1, slot);
+            bit_hsum(v[R - 1], b0, b1, slot);
+            xch[par][wi][0][lane] = t0;
+            xch[par][wi][1][lane] = t1;
+            xch[par][wi][2][lane] = b0;
+            xch[par][wi][3][lane] = b1;
+            if (HR == 0 || HR == R - 1) {
+                hdst[g * hstride + lane] = HR == 0 ? t0 : b0;
+                hdst[g * hstride + 64 + lane] = HR == 0 ? t1 : b1;
+            }
+            __syncthreads();
+            uint32_t a0 = 0u, a1 = 0u, d0 = 0u, d1 = 0u;
+            if (wi > 0) {
+                a0 = xch[par][wi - 1][2][lane];
+                a1 = xch[par][wi - 1][3][lane];
+            } else if (fed) {  // the previous window's row above this one
+                a0 = hist[hp][g][0][lane];
+                a1 = hist[hp][g][1][lane];
+            }
+            if (wi < NW - 1) {
+                d0 = xch[par][wi + 1][0][lane];
+                d1 = xch[par][wi + 1][1][lane];
+            }
+            uint32_t p0 = t0, p1 = t1, c0, c1;
+            bit_hsum(v[1], c0, c1, slot);
+            if (HR == 1) {
+                hdst[g * hstride + lane] = c0;
+                hdst[g * hstride + 64 + lane] = c1;
+            }
+            const uint32_t h10 = c0, h11 = c1;
+#pragma unroll
+            for (int r = 1; r < R - 1; ++r) {
+                uint32_t n0, n1;
+                if (r + 1 == R - 1) {
+                    n0 = b0;
+                    n1 = b1;
+                } else {
+                    bit_hsum(v[r + 1], n0, n1, slot);
+                    if (r + 1 == HR && HR > 1) {
+                        hdst[g * hstride + lane] = n0;
+                        hdst[g * hstride + 64 + lane] = n1;
+                    }
+                }
+                v[r] = BitEnc::rule1(p0, p1, c0, c1, n0, n1, v[r]);
+                p0 = c0;
+                p1 = c1;
+                c0 = n0;
+                c1 = n1;
+            }
+            v[R - 1] = BitEnc::rule1(p0, p1, b0, b1, d0, d1, v[R - 1]);
+            v[0] = BitEnc::rule1(a0, a1, t0, t1, h10, h11, v[0]);
+        }
+        // exact rows: [top + (fed ? 0 : K), top + NW*R - K), clipped to the segment
+        const int64_t lo = fed ? top : s0, hi0 = top + NW * R - K, hi = hi0 < s1 ? hi0 : s1;
+        uint8_t *q = a.out + (a.ya + y0) * a.pitch + voff;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int64_t yy = y0 + r;
+            if (st && yy >= lo && yy < hi && yy < a.h) {
+                if (BYTE) {
+                    uint4 *o = reinterpret_cast<uint4 *>(q);
+                    o[0] = make_uint4(unpack_nibble(v[r], 0), unpack_nibble(v[r], 1), unpack_nibble(v[r], 2),
+                                      unpack_nibble(v[r], 3));
+                    o[1] = make_uint4(unpack_nibble(v[r], 4), unpack_nibble(v[r], 5), unpack_nibble(v[r], 6),
+                                      unpack_nibble(v[r], 7));
+                } else {
+                    *reinterpret_cast<uint32_t *>(q) = v[r];
+                }
+            }
+            q += a.pitch;
+        }
+        if (hi >= s1) break;  // uniform: every wave leaves after the same window
+        top = hi0;
+    }
+}
+
 // ------------------------------------------------------------------ small grids
 // LDS-resident stencil for a grid that fits one CU (configs[1]: p46gun_big,
 // 500^2): one 1024-thread workgroup imports the shard into LDS as bits
@@ -1173,6 +1337,101 @@ hipError_t launch_k(const TArgs &a, Wrap wrap, unsigned grid, hipStream_t s) {
     }
 }
 }  // namespace
+
+namespace {
+template <bool BYTE, int R>
+hipError_t launch_c(const CArgs &a, Wrap wrap, unsigned grid, hipStream_t s) {
+    constexpr unsigned kThreads = 64 * kStackWaves;
+    if (wrap.x && wrap.y)
+        tchain_kernel<BYTE, R, 32, true, true><<<grid, kThreads, 0, s>>>(a);
+    else if (wrap.x)
+        tchain_kernel<BYTE, R, 32, true, false><<<grid, kThreads, 0, s>>>(a);
+    else if (wrap.y)
+        tchain_kernel<BYTE, R, 32, false, true><<<grid, kThreads, 0, s>>>(a);
+    else
+        tchain_kernel<BYTE, R, 32, false, false><<<grid, kThreads, 0, s>>>(a);
+    return hipGetLastError();
+}
+
+int device_cus() {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cus[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cus[dev] = n;
+    }
+    return cus[dev];
+}
+}  // namespace
+
+bool chain_supported(const life_layout &L) {
+    const int R = temporal_rows(is_bit(L));
+    return L.generations_per_exchange == 32 && (R == 32 || R == 48);
+}
+
+// Resident chained workgroups per CU of the instance a layout runs
+// (hipOccupancy: 3 for both encodings -- 6 waves per SIMD, 52 KiB of LDS each).
+template <bool BYTE, int R>
+int chain_per_cu() {
+    static const int n = [] {
+        int v = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, tchain_kernel<BYTE, R, 32, true, true>,
+                                                         64 * kStackWaves, 0) != hipSuccess || v <= 0)
+            v = 2;
+        return v;
+    }();
+    return n;
+}
+
+int chain_slots(const life_layout &L, int reserve) {
+    static const int env = [] {
+        const char *e = getenv("LIFE_CHAIN_SLOTS");
+        return e ? atoi(e) : 0;
+    }();
+    const bool bit = is_bit(L);
+    const int R = temporal_rows(bit);
+    const int per_cu = bit ? (R == 48 ? chain_per_cu<false, 48>() : chain_per_cu<false, 32>())
+                           : (R == 48 ? chain_per_cu<true, 48>() : chain_per_cu<true, 32>());
+    const int slots = env > 0 ? env : per_cu * device_cus();
+    return slots - reserve > 1 ? slots - reserve : 1;
+}
+
+hipError_t launch_tchain(const life_layout &L, const uint8_t *in, uint8_t *out, int64_t tx0, int64_t tx1,
+                         int64_t yb, int64_t ye, int m, Wrap wrap, int slots, hipStream_t s, double *windows) {
+    if (windows) *windows = 0.0;
+    if (!chain_supported(L) || m <= 0 || m > 32 || L.yapron != 32 || slots < 1) return hipErrorInvalidValue;
+    if (tx1 <= tx0 || ye <= yb) return hipSuccess;
+    const int64_t R = temporal_rows(is_bit(L)), K = 32;
+    const int64_t T1 = kStackWaves * R - 2 * K, T2 = kStackWaves * R - K;  // rows of a first / fed window
+    const int64_t rows = ye - yb, ncols = tx1 - tx0;
+    const int64_t nseg_max = slots / ncols > 1 ? slots / ncols : 1;
+    const int64_t per = (rows + nseg_max - 1) / nseg_max;
+    const int64_t nt = per <= T1 ? 1 : 1 + (per - T1 + T2 - 1) / T2;  // windows per full segment
+    const int64_t seg = T1 + (nt - 1) * T2;
+    const int64_t nseg = (rows + seg - 1) / seg;
+    const int64_t last = rows - (nseg - 1) * seg;
+    const int64_t nt_last = last <= T1 ? 1 : 1 + (last - T1 + T2 - 1) / T2;
+    if (windows) *windows = (double)ncols * (double)((nseg - 1) * nt + nt_last);
+    CArgs a;
+    a.in = in;
+    a.out = out;
+    a.pitch = L.pitch;
+    a.xoff = L.xoff;
+    a.W = (L.w + 31) / 32;
+    a.h = L.h;
+    a.ya = L.yapron;
+    a.tx0 = tx0;
+    a.ncols = ncols;
+    a.yb = yb;
+    a.ye = ye;
+    a.seg = seg;
+    a.m = m;
+    const unsigned grid = (unsigned)(ncols * nseg);
+    if (is_bit(L)) return R == 48 ? launch_c<false, 48>(a, wrap, grid, s) : launch_c<false, 32>(a, wrap, grid, s);
+    return R == 48 ? launch_c<true, 48>(a, wrap, grid, s) : launch_c<true, 32>(a, wrap, grid, s);
+}
 
 TileGeom tile_geom(const life_layout &L) {
     TileGeom g;

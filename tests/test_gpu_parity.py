@@ -76,9 +76,10 @@ def test_byte_equals_bit_long(gpu, oracle, nx):
     np.testing.assert_array_equal(out["bit"], oracle.life_run(g0, gens, threads=4))
 
 
+@pytest.mark.parametrize("chain", [False, True], ids=["tiles", "chain"])
 @pytest.mark.parametrize("kernel,nx,launches,gens", [("bit", 4096, 2, 40), ("bit", 31, 13, 13),
                                                      ("byte", 4096, 2, 40), ("byte", 31, 13, 13)])
-def test_timing_stats(gpu, kernel, nx, launches, gens):
+def test_timing_stats(gpu, kernel, nx, launches, gens, chain):
     """One timed launch per generation (one-generation kernels: a block
     narrower than the 32-cell apron) or per up to K generations (temporal
     kernels).  Bytes are the compulsory HBM
@@ -86,7 +87,7 @@ def test_timing_stats(gpu, kernel, nx, launches, gens):
     cells x generations; VALU lane-ops are modelled for the temporal kernel
     only (13 per register row per generation: the 14th op, the right
     neighbour fetch, runs on the LDS pipe)."""
-    with gpu.Life(nx, 4096, kernel=kernel, small_grid=False) as life:
+    with gpu.Life(nx, 4096, kernel=kernel, small_grid=False, chain=chain) as life:
         life.fill_random(1)
         life.set_timing(True)
         life.step(gens)
@@ -97,7 +98,7 @@ def test_timing_stats(gpu, kernel, nx, launches, gens):
         assert n * upd == pytest.approx(nx * 4096 * gens)
         temporal = launches < gens
         assert (valu > 0) == temporal
-        if temporal:  # 3 x ceil(4096 / (8 waves x R rows - 2K)) tiles of 62 words, 64 lanes;
+        if temporal and not chain:  # 3 x ceil(4096 / (8 waves x R rows - 2K)) tiles of 62 words, 64 lanes;
             # byte: + pack/unpack (35 ops per register row per launch)
             R, K = gpu.TEMPORAL_ROWS[kernel], gpu.TEMPORAL_DEPTH[kernel]
             tiles = 3 * -(-4096 // (8 * R - 2 * K))
@@ -110,13 +111,17 @@ def test_timing_stats(gpu, kernel, nx, launches, gens):
 @pytest.mark.parametrize("nx,ny", [(32, 1), (32, 5), (64, 64), (96, 33), (2048, 100), (1024, 1000), (4096, 48),
                                    (32, 200), (1984, 130), (2016, 7),
                                    # widths not a multiple of 32: the shard wraps its own x-aprons
-                                   (33, 9), (63, 64), (500, 500), (1000, 37), (4016, 130), (1985, 3), (2047, 200)])
-def test_temporal_single_shard(gpu, oracle, kernel, nx, ny):
+                                   (33, 9), (63, 64), (500, 500), (1000, 37), (4016, 130), (1985, 3), (2047, 200),
+                                   (256, 5000), (100, 3001)])
+@pytest.mark.parametrize("chain", [False, 3], ids=["tiles", "chain"])
+def test_temporal_single_shard(gpu, oracle, kernel, nx, ny, chain):
     """Blocks at least 32 cells wide take the temporally blocked kernel (up to
-    K generations per launch); runs of 1, 7, 8, 9, 20 and 40 generations."""
+    K generations per launch); runs of 1, 7, 8, 9, 20 and 40 generations.
+    tiles: independent tiles; chain: chained windows with 3 workgroups per
+    launch, so every tile column is walked by one or few long chains."""
     assert gpu.layout_query(nx, ny, (1, 1), 0, kernel).generations_per_exchange == gpu.TEMPORAL_DEPTH[kernel]
     g0 = oracle.fill_random(nx, ny, seed=nx + 3 * ny, density=0.5)
-    with gpu.Life(nx, ny, kernel=kernel, small_grid=False) as life:
+    with gpu.Life(nx, ny, kernel=kernel, small_grid=False, chain=chain) as life:
         life.upload(g0)
         done = 0
         for n in (1, 7, 8, 9, 20, 40):
@@ -133,7 +138,8 @@ def test_temporal_single_shard(gpu, oracle, kernel, nx, ny):
     (500, 500, 2, (2, 1)), (500, 300, 8, (4, 2)), (100, 64, 6, (3, 2)), (1000, 70, 4, (2, 2)), (2047, 90, 2, (1, 2)),
 ])
 @pytest.mark.parametrize("kernel", ["bit", "byte"])
-def test_temporal_multi_shard_local(gpu, oracle, kernel, nx, ny, shards, dims):
+@pytest.mark.parametrize("chain", [False, True, 2], ids=["tiles", "chain", "chain2"])
+def test_temporal_multi_shard_local(gpu, oracle, kernel, nx, ny, shards, dims, chain):
     """K-deep aprons through the LOCAL transport: whole-word columns, K-row
     blocks of rows, ring tiles first, interior overlapped with the exchange."""
     for r in range(shards):
@@ -141,7 +147,7 @@ def test_temporal_multi_shard_local(gpu, oracle, kernel, nx, ny, shards, dims):
         want = K if dims[1] == 1 or ny // dims[1] >= K else 1
         assert gpu.layout_query(nx, ny, dims, r, kernel).generations_per_exchange == want
     g0 = oracle.fill_random(nx, ny, seed=7 * shards + ny, density=0.45)
-    with gpu.Life(nx, ny, shards=shards, kernel=kernel, dims=dims, transport=gpu.XPORT_LOCAL) as life:
+    with gpu.Life(nx, ny, shards=shards, kernel=kernel, dims=dims, transport=gpu.XPORT_LOCAL, chain=chain) as life:
         life.upload(g0)
         done = 0
         for n in (1, 8, 13, 16, 30, 40):
