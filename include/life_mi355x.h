@@ -225,6 +225,17 @@ int life_dev_set_timing(life_dev *d, int on);
  * windows in lockstep, so the whole chip loads, then computes, and the load
  * phase the independent tiles hide is exposed. */
 #define LIFE_OPT_CHAIN 3
+/* LIFE_OPT_SMALL_GRID value 3: the register-resident small-grid kernel
+ * WINDOWED over several CUs whenever the shape allows
+ * (life_kernels.hip rsmall_kernel<.., WIN>): ceil(h / own) workgroups, each
+ * holding its own rows plus K halo rows above and below for K generations
+ * per launch; value 1 (default) windows only grids whose one-workgroup strips
+ * would be 4 or more rows tall (p46gun_big).  LIFE_OPT_SMALL_WINDOW sets the
+ * strip height R and K as value = R * 256 + K (R in 1..6 or 8, K <= 255;
+ * default automatic: R = 1, K = min(30, (strips - 8) / 2)).  Shapes it does
+ * not fit run as value 1 without the window.  Value 4: as 1, never
+ * windowed (the one-workgroup kernel; tests). */
+#define LIFE_OPT_SMALL_WINDOW 4
 int life_dev_configure(life_dev *d, int option, int value);
 int life_dev_kernel_stats(life_dev *d, double *avg_ms, int64_t *launches, double *bytes_per_launch);
 /* The same timed launches: mean cell-updates per launch (cells x generations

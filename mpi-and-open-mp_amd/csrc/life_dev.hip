@@ -102,7 +102,9 @@ struct life_dev {
     bool overlap = true;
     bool chain = false;   // chained temporal tiles where supported (LIFE_OPT_CHAIN; measured slower, off)
     int chain_slots = 0;  // > 0: workgroups per chained launch (tests: long chains on small grids)
-    int small_mode = 1;  // grids that fit one CU: 0 off, 1 VGPR kernel else LDS kernel, 2 LDS kernel
+    int small_mode = 1;  // grids that fit one CU: 0 off, 1 VGPR kernel else LDS kernel, 2 LDS kernel,
+                        // 3 windowed VGPR kernel over several CUs (else as 1), 4 as 1 never windowed
+    int win_rows = 0, win_halo = 0;  // windowed kernel: strip height R, halo rows K (0: automatic)
     std::vector<Shard> shards;
     double acc_ms = 0.0;
     int64_t acc_launches = 0;
@@ -732,10 +734,22 @@ int life_dev_fill_random(life_dev *d, uint64_t seed, uint32_t thr32) {
 
 // A single-shard grid small enough for one CU's LDS runs every generation of
 // the call in one resident-workgroup launch (life_kernels.hip, small_kernel).
+// Mode 1 (default) windows the VGPR kernel over several CUs when one
+// workgroup would need strips of 4 rows or more (p46gun_big 500^2: 10 rows,
+// 212 -> 632 Gcell/s windowed); mode 3 windows whenever the shape allows.
+static life::RegWinPlan win_plan(const life_dev *d) {
+    const life_layout &L = d->shards[0].lay;
+    if (d->small_mode == 3 || (d->small_mode == 1 && life::reg_small_rows(L) >= 4))
+        return life::reg_win_plan(L, d->win_rows, d->win_halo);
+    return life::RegWinPlan{};
+}
+
 static bool small_grid(const life_dev *d) {
     if (d->world != 1 || d->shards.size() != 1 || d->small_mode == 0) return false;
     const life_layout &L = d->shards[0].lay;
-    return (d->small_mode == 1 && life::reg_small_rows(L) > 0) || life::small_lds_bytes(L) <= life::kSmallMaxLds;
+    if (win_plan(d).blocks > 0) return true;
+    return (d->small_mode != 2 && life::reg_small_rows(L) > 0) ||
+           life::small_lds_bytes(L) <= life::kSmallMaxLds;
 }
 
 static int step_small(life_dev *d, int64_t generations) {
@@ -748,18 +762,30 @@ static int step_small(life_dev *d, int64_t generations) {
         if (!t) return rc;
         HIPCHK(hipEventRecord(t->a, s.stream));
     }
-    if (d->small_mode == 1 && life::reg_small_rows(s.lay) > 0)
-        HIPCHK(life::launch_reg_small(s.lay, s.buf[s.cur], s.buf[s.cur ^ 1], generations, s.stream));
-    else
-        HIPCHK(life::launch_small(s.lay, s.buf[s.cur], s.buf[s.cur ^ 1], generations, s.stream));
+    const life::RegWinPlan wp = win_plan(d);
+    int64_t passes = 1;  // HBM round trips of the grid
+    if (wp.blocks > 0) {
+        // K generations per launch, buffers swapped per launch
+        passes = 0;
+        for (int64_t g = 0; g < generations; g += wp.K, ++passes) {
+            const int m = (int)(generations - g < wp.K ? generations - g : wp.K);
+            HIPCHK(life::launch_reg_win(s.lay, wp, s.buf[s.cur], s.buf[s.cur ^ 1], m, s.stream));
+            s.cur ^= 1;
+        }
+    } else {
+        if (d->small_mode != 2 && life::reg_small_rows(s.lay) > 0)
+            HIPCHK(life::launch_reg_small(s.lay, s.buf[s.cur], s.buf[s.cur ^ 1], generations, s.stream));
+        else
+            HIPCHK(life::launch_small(s.lay, s.buf[s.cur], s.buf[s.cur ^ 1], generations, s.stream));
+        s.cur ^= 1;
+    }
     if (t) {
         HIPCHK(hipEventRecord(t->b, s.stream));
-        // LDS-resident: HBM sees one import and one export of the grid per launch
+        // CU-resident: HBM sees one import and one export of the grid per launch
         const double cells = (double)s.lay.w * (double)s.lay.h;
-        d->acc_bytes += cells * (s.lay.kernel == LIFE_KERNEL_BIT ? 0.25 : 2.0);
+        d->acc_bytes += (double)passes * cells * (s.lay.kernel == LIFE_KERNEL_BIT ? 0.25 : 2.0);
         d->acc_updates += cells * (double)generations;
     }
-    s.cur ^= 1;
     return LIFE_OK;
 }
 
@@ -956,9 +982,16 @@ int life_dev_configure(life_dev *d, int option, int value) {
     CHK(life_dev_sync(d));
     switch (option) {
     case LIFE_OPT_SMALL_GRID:
-        if (value < 0 || value > 2) return LIFE_EINVAL;
+        if (value < 0 || value > 4) return LIFE_EINVAL;
         d->small_mode = value;
         return LIFE_OK;
+    case LIFE_OPT_SMALL_WINDOW: {
+        const int R = value >> 8, K = value & 255;
+        if (R < 1 || K < 1) return LIFE_EINVAL;
+        d->win_rows = R;
+        d->win_halo = K;
+        return LIFE_OK;
+    }
     case LIFE_OPT_OVERLAP: d->overlap = value != 0; return LIFE_OK;
     case LIFE_OPT_CHAIN:
         if (value < 0) return LIFE_EINVAL;

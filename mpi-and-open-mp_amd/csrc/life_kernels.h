@@ -94,6 +94,16 @@ hipError_t launch_small(const life_layout &L, const uint8_t *in, uint8_t *out, i
 int reg_small_rows(const life_layout &L);
 hipError_t launch_reg_small(const life_layout &L, const uint8_t *in, uint8_t *out, int64_t gens,
                             hipStream_t s);
+// Windowed register-resident variant over several CUs: ceil(h / own)
+// workgroups, each holding own + 2K rows (strip height R) in VGPRs for at
+// most K generations per launch; in != out.  reg_win_plan returns blocks == 0
+// when the shape does not allow it.
+struct RegWinPlan {
+    int R, K, ns, own, blocks;
+};
+RegWinPlan reg_win_plan(const life_layout &L, int R, int K);
+hipError_t launch_reg_win(const life_layout &L, const RegWinPlan &p, const uint8_t *in, uint8_t *out, int gens,
+                          hipStream_t s);
 
 // Column halo staging: pack writes the last xapron columns to slot 0 and the
 // first xapron columns to slot 1 (h rows each: 1 byte 0/1 per row for a cell

@@ -23,6 +23,7 @@
 //    the rule).
 #include "life_kernels.h"
 
+#include <algorithm>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -816,6 +817,13 @@ __global__ __launch_bounds__(kSmallThreads) void small_kernel(SArgs a) {
 // applies the rule to its R rows.  PATCH (w % 32 != 0): the x wrap crosses a
 // partial word, so cell w-1 is moved to bit 31 of word 0's left word and
 // cell 0 is put at bit q of the last word before the sums.
+//
+// WIN (windowed, several CUs): workgroup b owns rows [b*own, b*own + own) and
+// holds the window of ns*R = own + 2K rows starting K rows above them (y
+// periodic); the strips at the window's top and bottom take zeros from
+// outside, so after m <= K generations rows [K, K + own) of the window are
+// exact and only those are stored (in != out; the host runs ceil(gens / K)
+// launches, swapping buffers).  ceil(h / own) workgroups instead of one.
 constexpr int kRegThreads = 1024;
 constexpr int kRegMaxW = 64;
 
@@ -824,12 +832,17 @@ struct RArgs {
     uint8_t *out;
     int64_t pitch, xoff, ya;
     int32_t w, h, W, lgWp, gens, bit, ns;
+    int32_t own, K;  // WIN: owned rows per workgroup, halo rows above/below
 };
 
-template <int R, bool PATCH>
+template <int R, bool PATCH, bool WIN>
 __global__ __launch_bounds__(kRegThreads) void rsmall_kernel(RArgs a) {
-    __shared__ uint32_t xch[2][4][kRegThreads];  // [parity][top s0/s1, bottom s0/s1][thread]
+    // [parity][top s0/s1, bottom s0/s1][thread]; WIN: 64 zero slots behind the
+    // threads stand for the rows outside the window
+    __shared__ uint32_t xch[2][4][kRegThreads + (WIN ? 64 : 0)];
     const int t = threadIdx.x;
+    if (WIN && t < 64)
+        for (int q = 0; q < 8; ++q) xch[q >> 2][q & 3][kRegThreads + t] = 0u;  // ordered by the first barrier
     const int Wp = 1 << a.lgWp, W = a.W;
     const int j = t & (Wp - 1);  // word column
     const int st = t >> a.lgWp;  // strip
@@ -843,15 +856,26 @@ __global__ __launch_bounds__(kRegThreads) void rsmall_kernel(RArgs a) {
     const uint32_t lsh = j == 0 ? (uint32_t)((32 - q) & 31) : 0u;  // cell w-1 -> bit 31
     const uint32_t qs = (uint32_t)(q & 31);
     const int sa = st == 0 ? a.ns - 1 : st - 1, sb = st + 1 >= a.ns ? 0 : st + 1;
-    const int ta = ((sa << a.lgWp) + j) & (kRegThreads - 1), tb = ((sb << a.lgWp) + j) & (kRegThreads - 1);
+    int ta = ((sa << a.lgWp) + j) & (kRegThreads - 1), tb = ((sb << a.lgWp) + j) & (kRegThreads - 1);
+    if (WIN) {
+        if (st == 0) ta = kRegThreads + (j & 63);
+        if (st + 1 >= a.ns) tb = kRegThreads + (j & 63);
+    }
     const int y0 = st * R;
+    // WIN: owned row of window row 0 (may be negative: periodic in y)
+    const int64_t wy = WIN ? (int64_t)blockIdx.x * a.own - a.K : 0;
 
     uint32_t v[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         uint32_t x = 0;
         if (active) {
-            const uint8_t *row = a.in + (int64_t)(y0 + r + a.ya) * a.pitch + a.xoff;
+            int64_t gy = y0 + r;
+            if (WIN) {
+                gy = (wy + gy) % a.h;
+                if (gy < 0) gy += a.h;
+            }
+            const uint8_t *row = a.in + (gy + a.ya) * a.pitch + a.xoff;
             if (a.bit) {
                 x = reinterpret_cast<const uint32_t *>(row)[j];
             } else {
@@ -897,7 +921,13 @@ __global__ __launch_bounds__(kRegThreads) void rsmall_kernel(RArgs a) {
     if (!active) return;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        uint8_t *row = a.out + (int64_t)(y0 + r + a.ya) * a.pitch + a.xoff;
+        int64_t gy = y0 + r;
+        if (WIN) {
+            // window rows [K, K + own) that exist
+            if (gy < a.K || gy >= a.K + a.own || wy + gy >= a.h) continue;
+            gy += wy;
+        }
+        uint8_t *row = a.out + (gy + a.ya) * a.pitch + a.xoff;
         const uint32_t x = v[r] & keep;
         if (a.bit) {
             reinterpret_cast<uint32_t *>(row)[j] = x;
@@ -911,13 +941,13 @@ __global__ __launch_bounds__(kRegThreads) void rsmall_kernel(RArgs a) {
 // gives at most kRegThreads / Wp strips is used.
 constexpr int kRegRows[] = {1, 2, 3, 4, 5, 6, 8, 10, 12, 16, 20, 25, 32};
 
-template <bool PATCH>
-hipError_t launch_rs(const RArgs &a, int R, hipStream_t s) {
+template <bool PATCH, bool WIN>
+hipError_t launch_rs(const RArgs &a, int R, unsigned blocks, hipStream_t s) {
     // only the waves that own strips (the barrier counts the launched waves)
     const unsigned threads = (unsigned)((((int64_t)a.ns << a.lgWp) + 63) / 64 * 64);
     switch (R) {
 #define LIFE_RS(N) \
-    case N: rsmall_kernel<N, PATCH><<<1, threads, 0, s>>>(a); break;
+    case N: rsmall_kernel<N, PATCH, WIN><<<blocks, threads, 0, s>>>(a); break;
         LIFE_RS(1) LIFE_RS(2) LIFE_RS(3) LIFE_RS(4) LIFE_RS(5) LIFE_RS(6) LIFE_RS(8) LIFE_RS(10) LIFE_RS(12)
         LIFE_RS(16) LIFE_RS(20) LIFE_RS(25) LIFE_RS(32)
 #undef LIFE_RS
@@ -1505,7 +1535,63 @@ hipError_t launch_reg_small(const life_layout &L, const uint8_t *in, uint8_t *ou
     a.gens = (int32_t)gens;
     a.bit = is_bit(L) ? 1 : 0;
     a.ns = (int32_t)(L.h / R);
-    return L.w % 32 ? launch_rs<true>(a, R, s) : launch_rs<false>(a, R, s);
+    a.own = a.h;
+    a.K = 0;
+    return L.w % 32 ? launch_rs<true, false>(a, R, 1, s) : launch_rs<false, false>(a, R, 1, s);
+}
+
+// Windowed plan: strip height R, halo K, strips per window ns (ns*R = own +
+// 2K), owned rows per workgroup.  Zero when the grid is not a VGPR shape, or
+// too short for one window to leave owned rows to more than one workgroup.
+// R = 0: automatic, R = 1 and K = min(30, (ns - 8) / 2), i.e. 8 owned rows per
+// workgroup -- the p46gun_big sweep (profiles/r01/p46_window_*.jsonl): R = 1
+// beats R >= 2 at every K, and the rate rises with K up to 28-30 (a
+// generation costs one barrier's latency whatever the window holds, so
+// deeper halos mean fewer launches).
+RegWinPlan reg_win_plan(const life_layout &L, int R, int K) {
+    RegWinPlan p{};
+    const int64_t W = (L.w + 31) / 32;
+    if (W > kRegMaxW || L.h <= 0) return p;
+    int64_t Wp = 1;
+    while (Wp < W) Wp <<= 1;
+    const int64_t ns = kRegThreads / Wp;
+    if (R == 0) {
+        R = 1;
+        K = (int)std::min<int64_t>(30, (ns - 8) / 2);
+        if (K < 8) return p;
+    }
+    if (K < 1 || (R != 1 && R != 2 && R != 3 && R != 4 && R != 5 && R != 6 && R != 8)) return p;
+    const int64_t own = ns * R - 2 * K;
+    if (own < 1 || own >= L.h) return p;
+    p.R = R;
+    p.K = K;
+    p.ns = (int)ns;
+    p.own = (int)own;
+    p.blocks = (int)((L.h + own - 1) / own);
+    return p;
+}
+
+hipError_t launch_reg_win(const life_layout &L, const RegWinPlan &p, const uint8_t *in, uint8_t *out, int gens,
+                          hipStream_t s) {
+    if (p.blocks < 1 || gens < 1 || gens > p.K || in == out) return hipErrorInvalidValue;
+    RArgs a;
+    a.in = in;
+    a.out = out;
+    a.pitch = L.pitch;
+    a.xoff = L.xoff;
+    a.ya = L.yapron;
+    a.w = (int32_t)L.w;
+    a.h = (int32_t)L.h;
+    a.W = (int32_t)((L.w + 31) / 32);
+    a.lgWp = 0;
+    while ((1 << a.lgWp) < a.W) ++a.lgWp;
+    a.gens = gens;
+    a.bit = is_bit(L) ? 1 : 0;
+    a.ns = p.ns;
+    a.own = p.own;
+    a.K = p.K;
+    const unsigned b = (unsigned)p.blocks;
+    return L.w % 32 ? launch_rs<true, true>(a, p.R, b, s) : launch_rs<false, true>(a, p.R, b, s);
 }
 
 int64_t small_lds_bytes(const life_layout &L) {

@@ -39,7 +39,7 @@ KERNELS = {"byte": KERNEL_BYTE, "bit": KERNEL_BIT}
 XPORT_AUTO, XPORT_RCCL, XPORT_LOCAL = 0, 1, 2
 HALO_SEND, HALO_RECV, HALO_FILL = 0, 1, 2
 HALO_COLUMN, HALO_ROW = 0, 1
-OPT_SMALL_GRID, OPT_OVERLAP, OPT_CHAIN = 1, 2, 3
+OPT_SMALL_GRID, OPT_OVERLAP, OPT_CHAIN, OPT_SMALL_WINDOW = 1, 2, 3, 4
 # LIFE_TEMPORAL_DEPTH(_BYTE): generations per halo exchange of the temporal layouts
 TEMPORAL_DEPTH = {"bit": 32, "byte": 32}
 TEMPORAL_ROWS = {"bit": 48, "byte": 32}  # default register rows per wave of the temporal tiles
@@ -225,7 +225,7 @@ class Life:
 
     def __init__(self, nx: int, ny: int, shards: int = 1, kernel="bit", dims=(0, 0),
                  transport: int = XPORT_AUTO, small_grid: bool = True, overlap: bool = True, chain=None,
-                 _handle=None):
+                 window=None, _handle=None):
         self.nx, self.ny = int(nx), int(ny)
         self.kernel = kernel_id(kernel)
         self._h = ctypes.c_void_p()
@@ -235,10 +235,16 @@ class Life:
             _check(_lib().life_dev_create_ex(self.nx, self.ny, shards, dims[0], dims[1], self.kernel,
                                              transport, ctypes.byref(self._h)), "life_dev_create")
         # small_grid: True/"auto" (VGPR kernel when the shape allows, else LDS),
-        # "lds" (LDS kernel only), False (the streaming kernels)
-        mode = {True: 1, "auto": 1, "lds": 2, False: 0}[small_grid]
+        # "lds" (LDS kernel only), "window" (the VGPR kernel windowed over
+        # several CUs where the shape allows, else as True; True windows only
+        # shapes whose one-workgroup strips would be >= 4 rows tall), "vgpr1"
+        # (as True, never windowed), False (the streaming kernels);
+        # window=(R, K): the windowed kernel's strip height and halo rows
+        mode = {True: 1, "auto": 1, "lds": 2, "window": 3, "vgpr1": 4, False: 0}[small_grid]
         if mode != 1:
             self.configure(OPT_SMALL_GRID, mode)
+        if window is not None:
+            self.configure(OPT_SMALL_WINDOW, int(window[0]) * 256 + int(window[1]))
         if not overlap:
             self.configure(OPT_OVERLAP, 0)
         # chain: None (library default: independent tiles), True (chained

@@ -42,7 +42,7 @@ def test_pattern_every_frame(gpu, name, kernel, shards):
             life.step(1)
 
 
-@pytest.mark.parametrize("small", [False, "lds", True], ids=["stream", "lds", "vgpr"])
+@pytest.mark.parametrize("small", [False, "lds", True, "vgpr1"], ids=["stream", "lds", "vgpr", "vgpr1"])
 @pytest.mark.parametrize("kernel", ["byte", "bit"])
 def test_p46gun_big_gen10000(gpu, kernel, small):
     """configs[1] at full length: md5 28998c4b... (549 live) after 10000 generations."""

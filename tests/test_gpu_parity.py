@@ -173,7 +173,7 @@ def test_temporal_tile_heights_agree(gpu, oracle, kernel, rows):
 
 
 # ---------------------------------------------------------------- CU-resident small grids
-@pytest.mark.parametrize("small", ["lds", True], ids=["lds", "vgpr"])
+@pytest.mark.parametrize("small", ["lds", True, "vgpr1"], ids=["lds", "vgpr", "vgpr1"])
 @pytest.mark.parametrize("kernel", ["bit", "byte"])
 @pytest.mark.parametrize("nx,ny,gens", [(500, 500, 300), (1, 1, 5), (33, 2, 17), (31, 31, 40), (1000, 600, 50),
                                         (32768, 19, 9), (64, 3, 100), (97, 1, 12),
@@ -184,6 +184,25 @@ def test_temporal_tile_heights_agree(gpu, oracle, kernel, rows):
 def test_small_grid_path(gpu, oracle, kernel, nx, ny, gens, small):
     g0 = oracle.fill_random(nx, ny, seed=nx ^ ny, density=0.4)
     with gpu.Life(nx, ny, kernel=kernel, small_grid=small) as life:
+        life.upload(g0)
+        life.step(gens)
+        np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, gens, threads=4))
+        life.step(1)
+        np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, gens + 1, threads=4))
+
+
+@pytest.mark.parametrize("kernel", ["bit", "byte"])
+@pytest.mark.parametrize("nx,ny,gens,window", [
+    (500, 500, 300, None), (500, 500, 77, (4, 32)), (500, 500, 40, (1, 3)),   # p46gun_big's shape
+    (64, 1000, 45, None), (2048, 512, 21, None), (1000, 600, 50, None),        # automatic R / K
+    (2047, 480, 19, (1, 4)), (1984, 400, 25, (2, 8)), (64, 1000, 45, (1, 100)),
+    (300, 100, 77, (1, 16)), (1000, 600, 50, (3, 20)), (96, 125, 64, (1, 70)), (10, 10, 33, None)])
+def test_small_grid_windowed(gpu, oracle, kernel, nx, ny, gens, window):
+    """The VGPR small-grid kernel windowed over ceil(h / own) workgroups
+    (K halo rows, K generations per launch; last window partial; shapes it
+    does not fit, like 10x10, fall back to the one-workgroup kernel)."""
+    g0 = oracle.fill_random(nx, ny, seed=nx ^ ny ^ 5, density=0.4)
+    with gpu.Life(nx, ny, kernel=kernel, small_grid="window", window=window) as life:
         life.upload(g0)
         life.step(gens)
         np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, gens, threads=4))
