@@ -835,7 +835,11 @@ struct RArgs {
     int32_t own, K;  // WIN: owned rows per workgroup, halo rows above/below
 };
 
-template <int R, bool PATCH, bool WIN>
+// ROT16 (W == Wp == 16, rows of 481..512 cells, e.g. p46gun_big): a lane
+// group is exactly one 16-lane DPP row, so the periodic neighbour words come
+// from DPP row rotates on the VALU instead of two ds_bpermute round trips
+// through the LDS pipe per row and generation.
+template <int R, bool PATCH, bool WIN, bool ROT16 = false>
 __global__ __launch_bounds__(kRegThreads) void rsmall_kernel(RArgs a) {
     // [parity][top s0/s1, bottom s0/s1][thread]; WIN: 64 zero slots behind the
     // threads stand for the rows outside the window
@@ -885,8 +889,15 @@ __global__ __launch_bounds__(kRegThreads) void rsmall_kernel(RArgs a) {
         v[r] = x;
     }
     auto hsum = [&](uint32_t c, uint32_t &s0, uint32_t &s1) {
-        uint32_t l = bperm(addr_l, c);
-        const uint32_t rw = bperm(addr_r, c);
+        uint32_t l;
+        uint32_t rw;
+        if (ROT16) {
+            l = (uint32_t)__builtin_amdgcn_mov_dpp((int)c, 0x121, 0xf, 0xf, false);   // row_ror:1 -> lane j-1
+            rw = (uint32_t)__builtin_amdgcn_mov_dpp((int)c, 0x12F, 0xf, 0xf, false);  // row_ror:15 -> lane j+1
+        } else {
+            l = bperm(addr_l, c);
+            rw = bperm(addr_r, c);
+        }
         if (PATCH) {
             l <<= lsh;
             // (c & keep) | (rw << qs & ~keep): the last word gets cell 0 at bit q (above it: don't-care)
@@ -945,6 +956,10 @@ template <bool PATCH, bool WIN>
 hipError_t launch_rs(const RArgs &a, int R, unsigned blocks, hipStream_t s) {
     // only the waves that own strips (the barrier counts the launched waves)
     const unsigned threads = (unsigned)((((int64_t)a.ns << a.lgWp) + 63) / 64 * 64);
+    if (WIN && R == 1 && a.W == 16 && a.lgWp == 4) {  // the automatic window shape, 16-word rows
+        rsmall_kernel<1, PATCH, WIN, true><<<blocks, threads, 0, s>>>(a);
+        return hipGetLastError();
+    }
     switch (R) {
 #define LIFE_RS(N) \
     case N: rsmall_kernel<N, PATCH, WIN><<<blocks, threads, 0, s>>>(a); break;
@@ -1543,9 +1558,9 @@ hipError_t launch_reg_small(const life_layout &L, const uint8_t *in, uint8_t *ou
 // Windowed plan: strip height R, halo K, strips per window ns (ns*R = own +
 // 2K), owned rows per workgroup.  Zero when the grid is not a VGPR shape, or
 // too short for one window to leave owned rows to more than one workgroup.
-// R = 0: automatic, R = 1 and K = min(30, (ns - 8) / 2), i.e. 8 owned rows per
+// R = 0: automatic, R = 1 and K = min(30, (ns - 4) / 2), i.e. 4 owned rows per
 // workgroup -- the p46gun_big sweep (profiles/r01/p46_window_*.jsonl): R = 1
-// beats R >= 2 at every K, and the rate rises with K up to 28-30 (a
+// beats R >= 2 at every K, and the rate rises with K up to 30 (a
 // generation costs one barrier's latency whatever the window holds, so
 // deeper halos mean fewer launches).
 RegWinPlan reg_win_plan(const life_layout &L, int R, int K) {
@@ -1557,7 +1572,7 @@ RegWinPlan reg_win_plan(const life_layout &L, int R, int K) {
     const int64_t ns = kRegThreads / Wp;
     if (R == 0) {
         R = 1;
-        K = (int)std::min<int64_t>(30, (ns - 8) / 2);
+        K = (int)std::min<int64_t>(30, (ns - 4) / 2);
         if (K < 8) return p;
     }
     if (K < 1 || (R != 1 && R != 2 && R != 3 && R != 4 && R != 5 && R != 6 && R != 8)) return p;

@@ -195,6 +195,7 @@ def test_small_grid_path(gpu, oracle, kernel, nx, ny, gens, small):
 @pytest.mark.parametrize("nx,ny,gens,window", [
     (500, 500, 300, None), (500, 500, 77, (4, 32)), (500, 500, 40, (1, 3)),   # p46gun_big's shape
     (64, 1000, 45, None), (2048, 512, 21, None), (1000, 600, 50, None),        # automatic R / K
+    (512, 300, 50, None), (481, 97, 33, None), (500, 64, 20, (1, 8)),          # 16-word rows: DPP row rotates
     (2047, 480, 19, (1, 4)), (1984, 400, 25, (2, 8)), (64, 1000, 45, (1, 100)),
     (300, 100, 77, (1, 16)), (1000, 600, 50, (3, 20)), (96, 125, 64, (1, 70)), (10, 10, 33, None)])
 def test_small_grid_windowed(gpu, oracle, kernel, nx, ny, gens, window):
