@@ -212,6 +212,25 @@ def test_small_grid_windowed(gpu, oracle, kernel, nx, ny, gens, window):
 
 
 @pytest.mark.parametrize("kernel", ["bit", "byte"])
+def test_small_grid_windowed_timing(gpu, oracle, kernel):
+    """Kernel stats of the windowed path: one event pair per step call,
+    counted as its ceil(gens / K) launches (automatic K = 30 for 16-word
+    rows), one grid import + export of HBM bytes per launch."""
+    nx, ny, gens = 500, 500, 95
+    g0 = oracle.fill_random(nx, ny, seed=46, density=0.4)
+    with gpu.Life(nx, ny, kernel=kernel) as life:
+        life.upload(g0)
+        life.set_timing(True)
+        life.step(gens)
+        ms, n, b = life.kernel_stats()
+        upd, _ = life.kernel_work()
+        assert n == 4 and ms > 0  # 30 + 30 + 30 + 5
+        assert n * b == pytest.approx(nx * ny * 4 * (0.25 if kernel == "bit" else 2.0))
+        assert n * upd == pytest.approx(nx * ny * gens)
+        np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, gens, threads=4))
+
+
+@pytest.mark.parametrize("kernel", ["bit", "byte"])
 def test_repeated_gather_is_stable(gpu, oracle, kernel):
     """Host transfers: 12 gathers of a 16 MiB grid into fresh pageable buffers
     all equal the oracle (guards the blocking-copy rule of life_dev_gather)."""
