@@ -384,6 +384,51 @@ __device__ __forceinline__ void bit_hsum(uint32_t v, uint32_t &s0, uint32_t &s1,
     BitEnc::fa(L, v, R, s0, s1);
 }
 
+// Drifting frame (LIFE_DRIFT, default 1): the temporal kernel computes the
+// next generation of cell x-1 at the bit that held cell x, so a row's sums
+// need only LEFT neighbours: with P the row's bits, hsum at p = P[p-2] +
+// P[p-1] + P[p] = LL + L + v (L = v << 1 | left >> 31, LL = v << 2 | left >>
+// 30), and the cell's own state is L.  The frame moves one bit left per
+// generation, all rows alike; after m generations bit p holds cell p - m and
+// the store realigns once per launch (alignbit with the right lane's word).
+// The right neighbour fetch and its shift disappear: 12 VALU + 1 ds_bpermute
+// per row instead of 13 VALU + 1 ds_bpermute.  Light cone: after m <= 32 generations positions [2m, 2048)
+// of the 64-lane row are exact, i.e. words 1..62 after realignment, the same
+// owned lanes as the centred frame.
+//
+// Measured (profiles/r01/drift_ab.jsonl, three interleaved rounds, 65536^2):
+// byte 61.5-61.9 -> 62.7-63.0 Tcell/s, bit 89.1-90.7 -> 88.4-89.1 (the VALU
+// count drop does not pay there); the left word by DPP instead (13 VALU, no
+// LDS) lost 5 % on both.  LIFE_DRIFT: 0 off, 1 (default) BYTE only, 2 both.
+#ifndef LIFE_DRIFT
+#define LIFE_DRIFT 1
+#endif
+constexpr bool kDrift[2] = {LIFE_DRIFT == 2, LIFE_DRIFT >= 1};  // [BIT, BYTE]
+__device__ __forceinline__ void bit_hsum_drift(uint32_t v, uint32_t &s0, uint32_t &s1, uint32_t &L) {
+    const uint32_t l = bperm((((int)__lane_id() - 1) & 63) << 2, v);
+    L = __builtin_amdgcn_alignbit(v, l, 31);
+    const uint32_t LL = __builtin_amdgcn_alignbit(v, l, 30);
+    BitEnc::fa(LL, L, v, s0, s1);
+}
+// the row sums in either frame; L: the cells the rule updates (v itself in
+// the centred frame)
+template <bool DRIFT>
+__device__ __forceinline__ void hsum_any(uint32_t v, uint32_t &s0, uint32_t &s1, uint32_t &L, uint32_t *slot) {
+    if (DRIFT) {
+        bit_hsum_drift(v, s0, s1, L);
+    } else {
+        bit_hsum(v, s0, s1, slot);
+        L = v;
+    }
+}
+// after m generations in the drifting frame: the aligned word of this lane's
+// column (bits m..31 of this lane, 0..m-1 of the right lane)
+__device__ __forceinline__ uint32_t drift_realign(uint32_t v, int m) {
+    const uint32_t r = bperm((((int)__lane_id() + 1) & 63) << 2, v);
+    if (m == 0) return v;
+    return m >= 32 ? r : __builtin_amdgcn_alignbit(r, v, (uint32_t)m);
+}
+
 // BYTE encoding through the same tiles: a lane's word column is 32 byte cells
 // (two 16-B loads per row), packed into one word on load (v_dot4_u32_u8
 // weights 1..128 per byte pair) and unpacked on store (nibble x 0x204081).
@@ -405,6 +450,7 @@ __global__ __launch_bounds__(64 * kStackWaves, 4) void tstep_kernel(TArgs a) {  
     constexpr int NW = kStackWaves;
     constexpr int T = NW * R - 2 * K;
     __shared__ uint32_t xch[2][NW][4][64];  // [parity][wave][top s0/s1, bottom s0/s1][lane]
+    constexpr bool DRIFT = kDrift[BYTE ? 1 : 0];
     const int lane = threadIdx.x & 63;
     // wave index: uniform, so every row address below is scalar (SALU) math
     const int wi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -482,9 +528,9 @@ __global__ __launch_bounds__(64 * kStackWaves, 4) void tstep_kernel(TArgs a) {  
     }
     for (int g = 0; g < a.m; ++g) {
         const int par = g & 1;
-        uint32_t t0, t1, b0, b1;
-        bit_hsum(v[0], t0, t1, slot);
-        bit_hsum(v[R - 1], b0, b1, slot);
+        uint32_t t0, t1, b0, b1, tL, bL;  // xL: the row's own cells in the frame used
+        hsum_any<DRIFT>(v[0], t0, t1, tL, slot);
+        hsum_any<DRIFT>(v[R - 1], b0, b1, bL, slot);
         xch[par][wi][0][lane] = t0;
         xch[par][wi][1][lane] = t1;
         xch[par][wi][2][lane] = b0;
@@ -502,26 +548,28 @@ __global__ __launch_bounds__(64 * kStackWaves, 4) void tstep_kernel(TArgs a) {  
         }
         // rows 1 .. R-2 need only this wave's rows: they run while the LDS
         // reads are in flight
-        uint32_t p0 = t0, p1 = t1, c0, c1;
-        bit_hsum(v[1], c0, c1, slot);
+        uint32_t p0 = t0, p1 = t1, c0, c1, cL;
+        hsum_any<DRIFT>(v[1], c0, c1, cL, slot);
         const uint32_t h10 = c0, h11 = c1;
 #pragma unroll
         for (int r = 1; r < R - 1; ++r) {
-            uint32_t n0, n1;
+            uint32_t n0, n1, nL;
             if (r + 1 == R - 1) {
                 n0 = b0;
                 n1 = b1;
+                nL = bL;
             } else {
-                bit_hsum(v[r + 1], n0, n1, slot);
+                hsum_any<DRIFT>(v[r + 1], n0, n1, nL, slot);
             }
-            v[r] = BitEnc::rule1(p0, p1, c0, c1, n0, n1, v[r]);
+            v[r] = BitEnc::rule1(p0, p1, c0, c1, n0, n1, cL);
+            cL = nL;
             p0 = c0;
             p1 = c1;
             c0 = n0;
             c1 = n1;
         }
-        v[R - 1] = BitEnc::rule1(p0, p1, b0, b1, d0, d1, v[R - 1]);
-        v[0] = BitEnc::rule1(a0, a1, t0, t1, h10, h11, v[0]);
+        v[R - 1] = BitEnc::rule1(p0, p1, b0, b1, d0, d1, bL);
+        v[0] = BitEnc::rule1(a0, a1, t0, t1, h10, h11, tL);
     }
     const bool st = lane >= 1 && lane <= 62 && j < a.W;
     // window rows [K, NW*R - K) are the tile's owned rows [ty*T, ty*T + T)
@@ -530,6 +578,7 @@ __global__ __launch_bounds__(64 * kStackWaves, 4) void tstep_kernel(TArgs a) {  
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         if (r < r0 || r >= r1) continue;
+        if (DRIFT) v[r] = drift_realign(v[r], a.m);  // every lane: the bpermute reads lane + 1
         if (st && y0 + r < a.h) {
             if (BYTE) {
                 uint4 *o = reinterpret_cast<uint4 *>(q);
@@ -1284,7 +1333,8 @@ int temporal_rows(bool bit) {
 // (8 x bfe/mul24/and) once per row and launch.
 constexpr double kValuPerRow = LIFE_HSUM_MODE == 0 ? 14.0 : LIFE_HSUM_MODE == 1 ? 12.0 : 13.0;
 double tstep_valu_per_tile_lane(int m, bool byte) {
-    return (double)kStackWaves * (double)temporal_rows(!byte) * (kValuPerRow * (double)m + (byte ? 35.0 : 0.0));
+    const double per_row = kDrift[byte ? 1 : 0] ? 12.0 : kValuPerRow;  // drifting frame: 12
+    return (double)kStackWaves * (double)temporal_rows(!byte) * (per_row * (double)m + (byte ? 35.0 : 0.0));
 }
 
 void set_temporal_rows(int kernel, int nr) {

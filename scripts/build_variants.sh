@@ -21,6 +21,8 @@ for v in "$@"; do
         nw16) build nw16 -DLIFE_STACK_WAVES=16 ;;
         nw4) build nw4 -DLIFE_STACK_WAVES=4 ;;
         xcd) build xcd -DLIFE_XCD_ORDER=1 ;;
+        drift0) build drift0 -DLIFE_DRIFT=0 ;;
+        drift2) build drift2 -DLIFE_DRIFT=2 ;;  # drifting frame for both encodings
         *) echo "unknown variant $v"; exit 1 ;;
     esac
 done

@@ -102,7 +102,8 @@ def test_timing_stats(gpu, kernel, nx, launches, gens, chain):
             # byte: + pack/unpack (35 ops per register row per launch)
             R, K = gpu.TEMPORAL_ROWS[kernel], gpu.TEMPORAL_DEPTH[kernel]
             tiles = 3 * -(-4096 // (8 * R - 2 * K))
-            per_row = 13 * gens + (35 * launches if kernel == "byte" else 0)  # 13 VALU + 1 LDS per row
+            # 13 VALU + 1 LDS per row; byte: drifting frame, 12 VALU + 1 LDS (life_kernels.hip LIFE_DRIFT)
+            per_row = (12 if kernel == "byte" else 13) * gens + (35 * launches if kernel == "byte" else 0)
             assert n * valu == pytest.approx(tiles * 64 * 8 * R * per_row)
 
 
