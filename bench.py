@@ -56,8 +56,13 @@ VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    # defaults: whole multiples of the temporal kernel's 32 generations per launch
-    p.add_argument("--steps", type=int, default=160)
+    # defaults: whole multiples of the temporal kernel's 32 generations per
+    # launch; one untimed launch, then generations 32..1024 of the random soup
+    # (configs[2]/[4] run 1000 generations from the random start).  Launches
+    # get faster as the soup thins out (65536^2 bit: 1.61 ms per launch at
+    # the start, 1.36 ms after ~10 launches, profiles/r01/bench_warmup.jsonl);
+    # timing the whole run, not only its cooled tail, keeps both in the rate.
+    p.add_argument("--steps", type=int, default=992)
     p.add_argument("--warmup", type=int, default=32)
     p.add_argument("--kernel", default="bit", choices=["bit", "byte"])
     p.add_argument("--size", type=int, default=65536, help="per-GPU block edge (weak scaling)")
