@@ -232,7 +232,7 @@ int life_dev_set_timing(life_dev *d, int on);
  * per launch; value 1 (default) windows only grids whose one-workgroup strips
  * would be 4 or more rows tall (p46gun_big).  LIFE_OPT_SMALL_WINDOW sets the
  * strip height R and K as value = R * 256 + K (R in 1..6 or 8, K <= 255;
- * default automatic: R = 1, K = min(30, (strips - 4) / 2)).  Shapes it does
+ * default and value 0: automatic, R = 1, K = min(30, (strips - 4) / 2)).  Shapes it does
  * not fit run as value 1 without the window.  Value 4: as 1, never
  * windowed (the one-workgroup kernel; tests). */
 #define LIFE_OPT_SMALL_WINDOW 4

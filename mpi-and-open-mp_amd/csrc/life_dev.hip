@@ -991,8 +991,8 @@ int life_dev_configure(life_dev *d, int option, int value) {
         d->small_mode = value;
         return LIFE_OK;
     case LIFE_OPT_SMALL_WINDOW: {
-        const int R = value >> 8, K = value & 255;
-        if (R < 1 || K < 1) return LIFE_EINVAL;
+        const int R = value >> 8, K = value & 255;  // R = 0 (value 0): automatic
+        if (value != 0 && (K < 1 || R < 1 || R > 8 || R == 7)) return LIFE_EINVAL;
         d->win_rows = R;
         d->win_halo = K;
         return LIFE_OK;
