@@ -212,6 +212,21 @@ def test_small_grid_windowed(gpu, oracle, kernel, nx, ny, gens, window):
         np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, gens + 1, threads=4))
 
 
+def test_small_grid_window_option_values(gpu, oracle):
+    """LIFE_OPT_SMALL_WINDOW: strip heights without a kernel instance and
+    K = 0 are rejected; value 0 restores the automatic plan."""
+    g0 = oracle.fill_random(500, 500, seed=3, density=0.4)
+    with gpu.Life(500, 500, small_grid="window") as life:
+        for bad in (7 * 256 + 5, 9 * 256 + 5, 1 * 256 + 0, 5):
+            with pytest.raises(gpu.LifeError):
+                life.configure(gpu.OPT_SMALL_WINDOW, bad)
+        life.configure(gpu.OPT_SMALL_WINDOW, 2 * 256 + 9)
+        life.configure(gpu.OPT_SMALL_WINDOW, 0)
+        life.upload(g0)
+        life.step(61)
+        np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, 61, threads=4))
+
+
 @pytest.mark.parametrize("kernel", ["bit", "byte"])
 def test_small_grid_windowed_timing(gpu, oracle, kernel):
     """Kernel stats of the windowed path: one event pair per step call,
