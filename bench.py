@@ -72,6 +72,8 @@ def parse():
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline sample budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--temporal", default="tiles", choices=["sweep", "tiles"],
+                   help="temporally blocked kernel: the tiled tstep_kernel (default) or sweep_kernel")
     p.add_argument("--rank-mode", action="store_true",
                    help="one-process-per-GPU set-up (gloo bootstrap, RCCL communicator) even at world 1")
     return p.parse_args()
@@ -152,6 +154,8 @@ def main():
         life = lm.Life.for_rank(nx, ny, rank, world, uid[0], local_rank, kernel=a.kernel, dims=dims)
     else:
         life = lm.Life(nx, ny, shards=a.gpus, kernel=a.kernel, dims=dims)
+    if a.temporal == "sweep":
+        life.configure(lm.OPT_SWEEP, 1)
 
     if grid is not None:
         life.upload(grid)

@@ -109,9 +109,9 @@ int life_halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int k
  * `generations_per_exchange` is how many generations one halo exchange
  * feeds: 1 for the one-cell apron; for the temporally blocked stencil
  * (32-cell x-apron, K-row y-apron) K = LIFE_TEMPORAL_DEPTH (bit) or
- * LIFE_TEMPORAL_DEPTH_BYTE (byte), or 16/24/32 from the environment variables
- * of the same names. */
-#define LIFE_TEMPORAL_DEPTH 32
+ * LIFE_TEMPORAL_DEPTH_BYTE (byte), or 8/12/16/24/32 from the environment
+ * variables of the same names. */
+#define LIFE_TEMPORAL_DEPTH 16
 #define LIFE_TEMPORAL_DEPTH_BYTE 32
 typedef struct {
     int64_t w, h;      /* owned block */
@@ -214,17 +214,13 @@ int life_dev_set_timing(life_dev *d, int on);
  * identical either way (tests switch them to reach every kernel). */
 #define LIFE_OPT_SMALL_GRID 1
 #define LIFE_OPT_OVERLAP 2
-/* LIFE_OPT_CHAIN (default 0): temporal layouts run chained tiles -- one
- * workgroup walks a segment of a tile column, each K-generation window fed
- * the exact row above it by the previous window (life_kernels.hip
- * tchain_kernel); 0: independent tiles (tstep_kernel); a value v > 1 also
- * sizes every chained launch to about v workgroups (default: 2 per CU), which
- * makes small grids walk long chains (tests).  Bit-exact, but measured
- * slower than independent tiles at 65536^2 (bit 0-10 %, byte 20-25 %,
- * profiles/r01/chain_sweep.jsonl): every chain starts together and walks its
- * windows in lockstep, so the whole chip loads, then computes, and the load
- * phase the independent tiles hide is exposed. */
-#define LIFE_OPT_CHAIN 3
+/* LIFE_OPT_SWEEP (default 0): 1 runs temporal layouts on the sweep stencil --
+ * one wave per column strip x row segment with the launch's m generations
+ * pipelined down the segment (life_sweep.hip); 0: the tiled
+ * stencil (8-wave workgroups holding a window of rows for all m
+ * generations, life_kernels.hip tstep_kernel), measured faster.  Same
+ * results either way. */
+#define LIFE_OPT_SWEEP 3
 /* LIFE_OPT_SMALL_GRID value 3: the register-resident small-grid kernel
  * WINDOWED over several CUs whenever the shape allows
  * (life_kernels.hip rsmall_kernel<.., WIN>): ceil(h / own) workgroups, each

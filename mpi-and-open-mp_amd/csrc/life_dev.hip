@@ -101,8 +101,8 @@ struct life_dev {
     bool rank_mode = false;
     bool timing = false;
     bool overlap = true;
-    bool chain = false;   // chained temporal tiles where supported (LIFE_OPT_CHAIN; measured slower, off)
-    int chain_slots = 0;  // > 0: workgroups per chained launch (tests: long chains on small grids)
+    bool sweep = false;  // temporal layouts: sweep_kernel (LIFE_OPT_SWEEP 1) or tstep_kernel tiles (0, default:
+                         // faster by measurement, profiles/r02/sweep_ab.txt)
     int small_mode = 1;  // grids that fit one CU: 0 off, 1 VGPR kernel else LDS kernel, 2 LDS kernel,
                         // 3 windowed VGPR kernel over several CUs (else as 1), 4 as 1 never windowed
     int win_rows = 0, win_halo = 0;  // windowed kernel: strip height R, halo rows K (0: automatic)
@@ -402,36 +402,6 @@ int launch_tiles(life_dev *d, Shard &s, const life::TileRegion *r, int nreg, int
     return LIFE_OK;
 }
 
-// Chained temporal tiles over tile columns [tx0, tx1) x owned rows [yb, ye)
-// (life::launch_tchain), with the same timing bookkeeping as launch_tiles.
-int launch_chain(life_dev *d, Shard &s, int64_t tx0, int64_t tx1, int64_t yb, int64_t ye, int m, int reserve,
-                 bool timed, hipStream_t st) {
-    const uint8_t *in = s.buf[s.cur];
-    uint8_t *out = s.buf[s.cur ^ 1];
-    TimedLaunch *t = nullptr;
-    if (d->timing && timed) {
-        int rc;
-        t = timer_slot(s, &rc);
-        if (!t) return rc;
-        HIPCHK(hipEventRecord(t->a, st));
-    }
-    double windows = 0.0;
-    const int slots = d->chain_slots > 0 ? d->chain_slots : life::chain_slots(s.lay, reserve);
-    HIPCHK(life::launch_tchain(s.lay, in, out, tx0, tx1, yb, ye, m, wrap_of(d), slots, st, &windows));
-    if (t) {
-        HIPCHK(hipEventRecord(t->b, st));
-        const life::TileGeom g = life::tile_geom(s.lay);
-        const int64_t xa = tx0 * g.words * 32, xb = std::min(tx1 * g.words * 32, s.lay.w);
-        const double cells = (double)(xb - xa) * (double)(std::min(ye, s.lay.h) - yb);
-        d->acc_bytes += cells * (s.lay.kernel == LIFE_KERNEL_BIT ? 0.25 : 2.0);
-        d->acc_updates += cells * (double)m;
-        d->acc_valu += windows * 64.0 * life::tstep_valu_per_tile_lane(m, s.lay.kernel == LIFE_KERNEL_BYTE);
-    }
-    return LIFE_OK;
-}
-
-bool use_chain(const life_dev *d, const Shard &s) { return d->chain && life::chain_supported(s.lay); }
-
 // Block boundary of the overlapped schedule: both compute streams wait for
 // the interior (stream2), the ring (stream) and the halo (comm stream).
 int join_streams(Shard &s) {
@@ -443,68 +413,129 @@ int join_streams(Shard &s) {
     return LIFE_OK;
 }
 
+// Sweep launch of up to 4 (strip, segment) regions on `st` (m generations,
+// cur -> nxt), optionally timed (life::launch_sweep).
+int launch_sweeps(life_dev *d, Shard &s, const life::SweepGeom &g, const life::TileRegion *r, int nreg, int m,
+                  bool timed, hipStream_t st) {
+    const uint8_t *in = s.buf[s.cur];
+    uint8_t *out = s.buf[s.cur ^ 1];
+    TimedLaunch *t = nullptr;
+    if (d->timing && timed) {
+        int rc;
+        t = timer_slot(s, &rc);
+        if (!t) return rc;
+        HIPCHK(hipEventRecord(t->a, st));
+    }
+    HIPCHK(life::launch_sweep(s.lay, g, in, out, r, nreg, m, wrap_of(d), st));
+    if (t) {
+        HIPCHK(hipEventRecord(t->b, st));
+        const bool byte = s.lay.kernel == LIFE_KERNEL_BYTE;
+        for (int k = 0; k < nreg; k++) {
+            // owned cells of the region: strips' owned columns x segments' rows
+            // (periodic x: [lo, hi) is the whole row shifted by edge - 32 cells)
+            const int64_t xa = std::max<int64_t>(32 * (r[k].tx0 * g.sw - 1) + g.edge, g.lo);
+            const int64_t xb = std::min<int64_t>(32 * (r[k].tx1 * g.sw - g.sw - 1) + 2048 - g.edge,
+                                                 g.lo < 0 ? g.hi : std::min<int64_t>(g.hi, s.lay.w));
+            const int64_t ya = r[k].ty0 * g.seg, yb = std::min(r[k].ty1 * g.seg, s.lay.h);
+            if (xb > xa && yb > ya) {
+                const double cells = (double)(xb - xa) * (double)(yb - ya);
+                d->acc_bytes += cells * (byte ? 2.0 : 0.25);
+                d->acc_updates += cells * (double)m;
+            }
+            d->acc_valu += 64.0 * life::sweep_valu_per_lane(g, r[k], s.lay.h, m, byte);
+        }
+    }
+    return LIFE_OK;
+}
+
+// Generations the next temporal launch runs (remaining > 0): sweep launches
+// split a step call into ceil(remaining / K) nearly equal launches of an
+// instantiated stage count; tiles run min(K, remaining).
+int next_block(const life_dev *d, int64_t remaining) {
+    const life_layout &L = d->shards[0].lay;
+    const int K = L.generations_per_exchange;
+    if (!d->sweep) return (int)std::min<int64_t>(remaining, K);
+    const int kmax = life::sweep_max_stages(L);
+    const int64_t n = (remaining + kmax - 1) / kmax;
+    const int target = (int)((remaining + n - 1) / n);
+    for (int m = target; m <= kmax && m <= remaining; ++m)
+        if (life::sweep_has(m)) return m;
+    for (int m = (int)std::min<int64_t>(remaining, kmax); m >= 1; --m)
+        if (life::sweep_has(m)) return m;
+    return 1;
+}
+
 // m <= K generations of the temporally blocked stencil on every shard, then
-// one K-deep halo exchange.  Partitioned shards: the boundary ring tiles
-// (one multi-region launch) run on the compute stream, the exchange of their
-// new state on the comm stream, and the interior tiles concurrently on the
-// second compute stream.  The ring holds every tile that produces a cell the
-// exchange sends: rows [0, K) and [h-K, h) (two tile rows at each end when the
-// last tile row is shorter than K), columns [0, 32) and [w-32, w) (the tile
-// column of word (w-32)/32 onwards when w % 32 != 0).  A self-wrapped x axis
-// (life::self_wrap_x) counts as partitioned: its "exchange" is the column copy.
+// one K-deep halo exchange.  Partitioned shards: the boundary ring (one
+// multi-region launch) runs on the compute stream, the exchange of its new
+// state on the comm stream, and the interior concurrently on the second
+// compute stream.  The ring holds every tile / (strip, segment) that produces
+// a cell the exchange sends: rows [0, K) and [h-K, h), columns [0, 32) and
+// [w-32, w).  A self-wrapped x axis (life::self_wrap_x) counts as
+// partitioned: its "exchange" is the column copy.
 int generation_block(life_dev *d, int m) {
     const bool rx = d->dims[0] > 1 || self_wrap_x(d), ry = d->dims[1] > 1;
-    if (!(rx || ry)) {
-        for (Shard &s : d->shards) {
-            HIPCHK(hipSetDevice(s.device));
-            const life::TileGeom g = life::tile_geom(s.lay);
-            if (use_chain(d, s)) {
-                CHK(launch_chain(d, s, 0, g.ntx, 0, s.lay.h, m, 0, true, s.stream));
-            } else {
-                const life::TileRegion all{0, g.ntx, 0, g.nty};
-                CHK(launch_tiles(d, s, &all, 1, m, true, s.stream));
-            }
-        }
-        for (Shard &s : d->shards) s.cur ^= 1;
-        return LIFE_OK;
-    }
     for (Shard &s : d->shards) {
         HIPCHK(hipSetDevice(s.device));
-        const life::TileGeom g = life::tile_geom(s.lay);
-        const int64_t TX = g.ntx, TY = g.nty, K = s.lay.generations_per_exchange;
-        // tile rows [0, ra) and [rb, TY), tile columns [0, ca) and [cb, TX)
-        int64_t ra = 0, rb = TY, ca = 0, cb = TX;
-        if (ry) {
-            ra = std::min((K + g.rows - 1) / g.rows, TY);
-            rb = std::max(std::min((s.lay.h - K) / g.rows, TY), ra);
+        const int64_t K = s.lay.generations_per_exchange;
+        // grid of units (tiles or strips x segments): NX x NY, unit height uh;
+        // column units [0, ca) and [cb, NX) hold the x-ring
+        int64_t NX, NY, uh, ca = 0, cb;
+        life::SweepGeom sg{};
+        if (d->sweep) {
+            sg = life::sweep_geom(s.lay, wrap_of(d).x);
+            NX = sg.nstrips;
+            NY = sg.nseg;
+            uh = sg.seg;
+            cb = NX;
+            if (rx) {
+                ca = 1;  // strip 0 owns [0, 2048 - 2 edge) >= [0, 32)
+                cb = 0;
+                while (cb < NX && 32 * (cb * sg.sw - 1) + 2048 - sg.edge <= s.lay.w - 32) ++cb;
+                cb = std::max(cb, ca);
+            }
+        } else {
+            const life::TileGeom g = life::tile_geom(s.lay);
+            NX = g.ntx;
+            NY = g.nty;
+            uh = g.rows;
+            cb = NX;
+            if (rx) {
+                ca = 1;
+                cb = std::max(std::min(((s.lay.w - 32) / 32) / g.words, NX), ca);
+            }
         }
-        if (rx) {
-            ca = 1;
-            cb = std::max(std::min(((s.lay.w - 32) / 32) / g.words, TX), ca);
+        auto launch = [&](const life::TileRegion *r, int n, bool timed, hipStream_t st) -> int {
+            return d->sweep ? launch_sweeps(d, s, sg, r, n, m, timed, st) : launch_tiles(d, s, r, n, m, timed, st);
+        };
+        if (!(rx || ry)) {
+            const life::TileRegion all{0, NX, 0, NY};
+            CHK(launch(&all, 1, true, s.stream));
+            continue;
+        }
+        // unit rows [0, ra) and [rb, NY), unit columns [0, ca) and [cb, NX)
+        int64_t ra = 0, rb = NY;
+        if (ry) {
+            ra = std::min((K + uh - 1) / uh, NY);
+            rb = std::max(std::min((s.lay.h - K) / uh, NY), ra);
         }
         life::TileRegion ring[4];
         int n = 0;
-        if (ra > 0) ring[n++] = life::TileRegion{0, TX, 0, ra};
-        if (rb < TY) ring[n++] = life::TileRegion{0, TX, rb, TY};
+        if (ra > 0) ring[n++] = life::TileRegion{0, NX, 0, ra};
+        if (rb < NY) ring[n++] = life::TileRegion{0, NX, rb, NY};
         if (rb > ra) {
             if (ca > 0) ring[n++] = life::TileRegion{0, ca, ra, rb};
-            if (cb < TX) ring[n++] = life::TileRegion{cb, TX, ra, rb};
+            if (cb < NX) ring[n++] = life::TileRegion{cb, NX, ra, rb};
         }
-        CHK(launch_tiles(d, s, ring, n, m, false, s.stream));
+        CHK(launch(ring, n, false, s.stream));
         HIPCHK(hipEventRecord(s.ev_ring, s.stream));
         HIPCHK(hipStreamWaitEvent(s.comm_stream, s.ev_ring, 0));
         const life::TileRegion inner{ca, cb, ra, rb};
-        if (rb > ra && cb > ca) {
-            if (use_chain(d, s)) {
-                // leave the slots of the concurrent ring tiles (and a few for RCCL) free
-                int64_t ring_tiles = 0;
-                for (int k = 0; k < n; k++) ring_tiles += (ring[k].tx1 - ring[k].tx0) * (ring[k].ty1 - ring[k].ty0);
-                CHK(launch_chain(d, s, ca, cb, ra * g.rows, std::min(rb * g.rows, s.lay.h), m,
-                                 (int)std::min<int64_t>(ring_tiles + 8, 1 << 20), true, s.stream2));
-            } else {
-                CHK(launch_tiles(d, s, &inner, 1, m, true, s.stream2));
-            }
-        }
+        if (rb > ra && cb > ca) CHK(launch(&inner, 1, true, s.stream2));
+    }
+    if (!(rx || ry)) {
+        for (Shard &s : d->shards) s.cur ^= 1;
+        return LIFE_OK;
     }
     CHK(exchange(d, 1, true));
     for (Shard &s : d->shards) {
@@ -816,9 +847,11 @@ int life_dev_step(life_dev *d, int64_t generations) {
         return exchange(d, 0, false);
     }
     if (temporal(d)) {
-        const int K = d->shards[0].lay.generations_per_exchange;
-        for (int64_t g = 0; g < generations; g += K)
-            CHK(generation_block(d, (int)(generations - g < K ? generations - g : K)));
+        for (int64_t g = 0; g < generations;) {
+            const int m = next_block(d, generations - g);
+            CHK(generation_block(d, m));
+            g += m;
+        }
         return LIFE_OK;
     }
     for (int64_t g = 0; g < generations; g++) CHK(generation(d));
@@ -998,10 +1031,9 @@ int life_dev_configure(life_dev *d, int option, int value) {
         return LIFE_OK;
     }
     case LIFE_OPT_OVERLAP: d->overlap = value != 0; return LIFE_OK;
-    case LIFE_OPT_CHAIN:
-        if (value < 0) return LIFE_EINVAL;
-        d->chain = value != 0;
-        d->chain_slots = value > 1 ? value : 0;
+    case LIFE_OPT_SWEEP:
+        if (value < 0 || value > 1) return LIFE_EINVAL;
+        d->sweep = value != 0;
         return LIFE_OK;
     default: return LIFE_EINVAL;
     }

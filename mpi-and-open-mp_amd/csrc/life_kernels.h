@@ -49,6 +49,7 @@ void set_step_tuning(int kernel, int rows, int depth);  // kernel -1: both
 // Temporally blocked stencil (layouts with generations_per_exchange = K in
 // {8, 16}, either encoding): tiles of 62 32-cell word columns x `rows` rows
 // (one workgroup each), m <= K generations per launch from `in` to `out`.
+constexpr int kMaxRegions = 4;  // regions one temporal launch may hold
 struct TileRegion {
     int64_t tx0, tx1, ty0, ty1;
 };
@@ -64,22 +65,30 @@ constexpr int64_t kTemporalSlackRows = 8 * 96;
 hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, const TileRegion *r, int nreg,
                         int m, Wrap wrap, hipStream_t s);
 int temporal_rows(bool bit);      // register rows per wave (32/40/48/56/64/96)
-// Chained temporal tiles (tchain_kernel): the tile columns [tx0, tx1) x owned
-// rows [yb, ye) of a temporal layout, one workgroup per segment of a tile
-// column walking K-generation windows top to bottom (each window's top row
-// fed by the one above it).  Segments are sized so the launch is about
-// `slots` workgroups (chain_slots(L, reserve): the resident workgroups per CU
-// x CUs, minus `reserve` slots left to concurrent work).  *windows = windows
-// computed (VALU model).
-bool chain_supported(const life_layout &L);  // K = 32 and the tile height has an instance
-int chain_slots(const life_layout &L, int reserve);
-hipError_t launch_tchain(const life_layout &L, const uint8_t *in, uint8_t *out, int64_t tx0, int64_t tx1,
-                         int64_t yb, int64_t ye, int m, Wrap wrap, int slots, hipStream_t s, double *windows);
 // VALU instructions the lanes at one lane position of a tile's waves issue
 // for m generations (the op-count model of life_kernels.hip tstep_kernel,
 // checked against the SQ_INSTS_VALU counter in profiles/); x 64 lanes x tiles.
 double tstep_valu_per_tile_lane(int m, bool byte);
 void set_temporal_rows(int kernel, int nr);  // kernel -1: both encodings
+
+// Sweep stencil (sweep_kernel, the default temporal kernel): one wave per
+// column strip x row segment, m generations pipelined down the segment.
+// Strip s covers window words [s*sw - 1, s*sw + 63) and owns the window cells
+// [edge, 2048 - edge) of them inside [lo, hi); segments are `seg` owned rows.
+// Regions are TileRegions in (strip, segment) units.
+struct SweepGeom {
+    int edge;                // ghost cells per strip side: 16 (K <= 16) or 32
+    int64_t sw;              // strip stride in words (63 / 62)
+    int64_t lo, hi;          // owned cells of a row (whole words; periodic x: lo = edge - 32)
+    int64_t nstrips, seg, nseg;
+};
+SweepGeom sweep_geom(const life_layout &L, bool wrapx);
+int sweep_max_stages(const life_layout &L);  // generations one launch may run
+bool sweep_has(int m);                       // a kernel instance with m stages exists
+hipError_t launch_sweep(const life_layout &L, const SweepGeom &g, const uint8_t *in, uint8_t *out,
+                        const TileRegion *r, int nreg, int m, Wrap wrap, hipStream_t s);
+// VALU instructions one lane position of the region's waves issues (model).
+double sweep_valu_per_lane(const SweepGeom &g, const TileRegion &r, int64_t h, int m, bool byte);
 
 // LDS-resident path for small single-shard grids: all `gens` generations in
 // one single-workgroup launch (in -> out; in may equal out).  Usable when

@@ -22,6 +22,7 @@
 //    step is one v_bitop3_b32 (6 ops per row sum incl. 2 DPP moves, 8 for
 //    the rule).
 #include "life_kernels.h"
+#include "life_bitops.h"
 
 #include <algorithm>
 #include <stdint.h>
@@ -77,64 +78,6 @@ struct ByteEnc {
     }
 };
 
-// v_bitop3_b32 (gfx950): any 3-input bitwise function in one VALU op.  The
-// truth table is indexed by {S0,S1,S2} with S0 the most significant bit, so
-// the immediate of f is f(0xF0, 0xCC, 0xAA).
-template <uint32_t IMM>
-__device__ __forceinline__ uint32_t b3(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, IMM);
-}
-constexpr uint32_t kXor3 = 0xF0 ^ 0xCC ^ 0xAA;                          // a ^ b ^ c
-constexpr uint32_t kMaj = (0xF0 & 0xCC) | (0xF0 & 0xAA) | (0xCC & 0xAA);  // majority
-constexpr uint32_t kEq1 = ((0xF0 ^ 0xCC) & ~0xAA) & 0xFF;                // (v0^k0) & ~v1
-constexpr uint32_t kEq2 = (~(0xF0 ^ 0xCC) & (0xAA ^ (0xF0 & 0xCC))) & 0xFF;  // ~(v0^k0) & (v1^(v0&k0))
-constexpr uint32_t kMux = ((0xF0 & 0xCC) | (~0xF0 & 0xAA)) & 0xFF;       // a ? b : c
-constexpr uint32_t kAndOr = (0xF0 & (0xCC | 0xAA)) & 0xFF;               // a & (b | c)
-
-struct BitEnc {
-    static constexpr int64_t kCellsPerUnit = 128;
-    static constexpr uint32_t kCell0 = 1u;
-    static __device__ __forceinline__ int64_t dword_of(int64_t x) { return x >> 5; }
-    static __device__ __forceinline__ uint32_t pos_in_dword(int64_t x) { return (uint32_t)(x & 31); }
-    static __device__ __forceinline__ uint32_t top_shift(int64_t x) { return 31u - pos_in_dword(x); }
-    struct H {
-        uint32_t s0[4], s1[4];
-    };
-    // full adder: L + C + R = s0 + 2*s1
-    static __device__ __forceinline__ void fa(uint32_t L, uint32_t C, uint32_t R, uint32_t &s0,
-                                              uint32_t &s1) {
-        s0 = b3<kXor3>(L, C, R);
-        s1 = b3<kMaj>(L, C, R);
-    }
-    static __device__ __forceinline__ H hsum(uint4 d, uint32_t l, uint32_t r) {
-        H h;
-        fa(__builtin_amdgcn_alignbit(d.x, l, 31), d.x, __builtin_amdgcn_alignbit(d.y, d.x, 1), h.s0[0], h.s1[0]);
-        fa(__builtin_amdgcn_alignbit(d.y, d.x, 31), d.y, __builtin_amdgcn_alignbit(d.z, d.y, 1), h.s0[1], h.s1[1]);
-        fa(__builtin_amdgcn_alignbit(d.z, d.y, 31), d.z, __builtin_amdgcn_alignbit(d.w, d.z, 1), h.s0[2], h.s1[2]);
-        fa(__builtin_amdgcn_alignbit(d.w, d.z, 31), d.w, __builtin_amdgcn_alignbit(r, d.w, 1), h.s0[3], h.s1[3]);
-        return h;
-    }
-    // Rows a, b, c (2-bit horizontal sums) -> next state of the centre row.
-    // n9 = (a0+b0+c0) + 2(a1+b1+c1) = u0 + 2*S with S = v0 + k0 + 2*v1;
-    // alive' = (n9 == 3) | (alive & n9 == 4) = u0 ? S==1 : (alive & S==2).
-    static __device__ __forceinline__ uint32_t rule1(uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1,
-                                                     uint32_t c0, uint32_t c1, uint32_t alive) {
-        const uint32_t u0 = b3<kXor3>(a0, b0, c0), k0 = b3<kMaj>(a0, b0, c0);
-        const uint32_t v0 = b3<kXor3>(a1, b1, c1), v1 = b3<kMaj>(a1, b1, c1);
-        const uint32_t eq1 = b3<kEq1>(v0, k0, v1);  // S == 1
-        const uint32_t eq2 = b3<kEq2>(v0, k0, v1);  // S == 2
-        const uint32_t e = b3<kMux>(u0, eq1, eq2);
-        return b3<kAndOr>(e, u0, alive);  // u0 ? eq1 : (alive & eq2)
-    }
-    static __device__ __forceinline__ uint4 rule(const H &a, const H &b, const H &c, uint4 v) {
-        uint4 o;
-        o.x = rule1(a.s0[0], a.s1[0], b.s0[0], b.s1[0], c.s0[0], c.s1[0], v.x);
-        o.y = rule1(a.s0[1], a.s1[1], b.s0[1], b.s1[1], c.s0[1], c.s1[1], v.y);
-        o.z = rule1(a.s0[2], a.s1[2], b.s0[2], b.s1[2], c.s0[2], c.s1[2], v.z);
-        o.w = rule1(a.s0[3], a.s1[3], b.s0[3], b.s1[3], c.s0[3], c.s1[3], v.w);
-        return o;
-    }
-};
 
 // ------------------------------------------------------------------ stencil
 // Per-lane constants of one stencil launch.  Every load is unconditional (a
@@ -298,31 +241,17 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs a) {
 }
 
 // ------------------------------------------------------------------ temporal
-// Temporally blocked bit stencil (layouts with generations_per_exchange = K
-// > 1): m <= K generations per launch, each cell's bit read once from and
-// written once to HBM per launch.
+// Temporally blocked stencils (layouts with generations_per_exchange = K
+// > 1): m <= K generations per launch, each cell read once from and written
+// once to HBM per launch (plus the ghost rows of its window).  Two kernels:
 //
-// One workgroup owns a tile of 62 word columns x T owned rows.  Its
-// kStackWaves waves are stacked vertically: wave i holds window rows
-// [i*R, (i+1)*R) of a (kStackWaves*R)-row window that starts K rows above the
-// tile (T = kStackWaves*R - 2K), one 32-cell word per lane and register row
-// (lane l holds word column 62*tx + l - 1; lanes 0 and 63 are the one-word
-// x-apron of the tile).  Each generation a wave publishes the horizontal sums
-// of its first and last row in LDS, one barrier, and takes its neighbours'
-// (the only values that cross waves); the window's own top/bottom K rows and
-// the edge lanes absorb the wrong values that enter from outside (K rows / K
-// <= 32 bits after K generations), so rows [K, K+T) of lanes 1..62 are exact.
-// Versus one wave per tile (K-row ghost zones per wave), the ghost rows are
-// paid once per workgroup: 2K of kStackWaves*R rows.
-//
-// VALU (MI355X): per register row and generation 2 DPP moves + 2 v_alignbit
-// (horizontal neighbours) + 10 v_bitop3 (full adder 2, rule 8);
-// scripts/ubench_row.hip prices the row at ~20.7 ns per SIMD at 16 waves/CU.
-constexpr int kMaxRegions = 4;
-#ifndef LIFE_STACK_WAVES
-#define LIFE_STACK_WAVES 8
-#endif
-constexpr int kStackWaves = LIFE_STACK_WAVES;  // waves per workgroup (2 per SIMD)
+//  * sweep_kernel (default): one WAVE per column strip x row segment, the
+//    m generations pipelined down the segment (see below);
+//  * tstep_kernel: one 8-wave workgroup per 62-word x (8R - 2K)-row tile,
+//    all m generations of the tile in registers with one barrier per
+//    generation (LIFE_OPT_SWEEP 0).
+
+constexpr int kStackWaves = 8;  // tstep: waves per workgroup (2 per SIMD)
 struct TArgs {
     const uint8_t *in;
     uint8_t *out;
@@ -332,158 +261,56 @@ struct TArgs {
     int64_t tx0[kMaxRegions], tx1[kMaxRegions], ty0[kMaxRegions], ty1[kMaxRegions], first[kMaxRegions + 1];
     int32_t nreg, m;
 };
-#ifndef LIFE_XCD_ORDER
-#define LIFE_XCD_ORDER 0
-#endif
 
-// Neighbour words with bound_ctrl: lanes 0 / 63 read 0 (their outer bits are
-// allowed to be wrong), and the DPP move needs no `old` operand copy.
+// Neighbour word from the left lane (DPP wave_shr:1, bound_ctrl: lane 0 reads
+// 0 -- its outer bits are allowed to be wrong).
 __device__ __forceinline__ uint32_t left_or_zero(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xf, 0xf, true);
 }
-__device__ __forceinline__ uint32_t right_or_zero(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xf, 0xf, true);
-}
-
-// Where the neighbour words come from (build-time switch): 0: both DPP moves
-// (VALU); 1: both ds_bpermute (LDS pipe); 2 (default): DPP left, ds_bpermute
-// right -- the row is VALU-issue bound, and moving one of its 14 VALU
-// instructions to the otherwise idle LDS pipe measured +10 % (bit, K = 32:
-// 91.0 -> 99.8 Tcell/s at 65536^2; mode 1 lost 13 %: profiles/r01/hsum_modes.txt).
-#ifndef LIFE_HSUM_MODE
-#define LIFE_HSUM_MODE 2
-#endif
-__device__ __forceinline__ uint32_t bperm(int addr, uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)v);
-}
-// Mode 3: both neighbour words through a per-wave LDS row (one ds_write_b32,
-// one ds_read2_b32): LDS operations of one wave execute in issue order, so the
-// read sees the write without a wait; the signal fences keep the compiler
-// from reordering the row's LDS accesses (slot[0] and slot[65] stay 0).
-__device__ __forceinline__ void bit_hsum(uint32_t v, uint32_t &s0, uint32_t &s1, uint32_t *slot) {
-#if LIFE_HSUM_MODE == 3
-    const int lane = (int)__lane_id();
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    slot[lane + 1] = v;
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    const uint32_t l = slot[lane], r = slot[lane + 2];
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-#elif LIFE_HSUM_MODE == 0
-    const uint32_t l = left_or_zero(v), r = right_or_zero(v);
-#else
+// Centred-frame row sums (tstep, bit): the left word by DPP on the VALU, the
+// right one by ds_bpermute on the otherwise idle LDS pipe (+10 % over two DPP
+// moves, profiles/r01/hsum_modes.txt).  13 VALU + 1 LDS per row.
+__device__ __forceinline__ void bit_hsum(uint32_t v, uint32_t &s0, uint32_t &s1) {
     const int lane = (int)__lane_id();
     const uint32_t r = bperm(((lane + 1) & 63) << 2, v);
-#if LIFE_HSUM_MODE == 1
-    const uint32_t l = bperm(((lane - 1) & 63) << 2, v);
-#else
     const uint32_t l = left_or_zero(v);
-#endif
-#endif
     const uint32_t L = __builtin_amdgcn_alignbit(v, l, 31);
     const uint32_t R = __builtin_amdgcn_alignbit(r, v, 1);
     BitEnc::fa(L, v, R, s0, s1);
 }
 
-// Drifting frame (LIFE_DRIFT, default 1): the temporal kernel computes the
-// next generation of cell x-1 at the bit that held cell x, so a row's sums
-// need only LEFT neighbours: with P the row's bits, hsum at p = P[p-2] +
-// P[p-1] + P[p] = LL + L + v (L = v << 1 | left >> 31, LL = v << 2 | left >>
-// 30), and the cell's own state is L.  The frame moves one bit left per
-// generation, all rows alike; after m generations bit p holds cell p - m and
-// the store realigns once per launch (alignbit with the right lane's word).
-// The right neighbour fetch and its shift disappear: 12 VALU + 1 ds_bpermute
-// per row instead of 13 VALU + 1 ds_bpermute.  Light cone: after m <= 32 generations positions [2m, 2048)
-// of the 64-lane row are exact, i.e. words 1..62 after realignment, the same
-// owned lanes as the centred frame.
-//
-// Measured (profiles/r01/drift_ab.jsonl, three interleaved rounds, 65536^2):
-// byte 61.5-61.9 -> 62.7-63.0 Tcell/s, bit 89.1-90.7 -> 88.4-89.1 (the VALU
-// count drop does not pay there); the left word by DPP instead (13 VALU, no
-// LDS) lost 5 % on both.  LIFE_DRIFT: 0 off, 1 (default) BYTE only, 2 both.
-#ifndef LIFE_DRIFT
-#define LIFE_DRIFT 1
-#endif
-constexpr bool kDrift[2] = {LIFE_DRIFT == 2, LIFE_DRIFT >= 1};  // [BIT, BYTE]
-__device__ __forceinline__ void bit_hsum_drift(uint32_t v, uint32_t &s0, uint32_t &s1, uint32_t &L) {
-    const uint32_t l = bperm((((int)__lane_id() - 1) & 63) << 2, v);
-    L = __builtin_amdgcn_alignbit(v, l, 31);
-    const uint32_t LL = __builtin_amdgcn_alignbit(v, l, 30);
-    BitEnc::fa(LL, L, v, s0, s1);
-}
-// the row sums in either frame; L: the cells the rule updates (v itself in
-// the centred frame)
-template <bool DRIFT>
-__device__ __forceinline__ void hsum_any(uint32_t v, uint32_t &s0, uint32_t &s1, uint32_t &L, uint32_t *slot) {
-    if (DRIFT) {
-        bit_hsum_drift(v, s0, s1, L);
-    } else {
-        bit_hsum(v, s0, s1, slot);
-        L = v;
-    }
-}
-// after m generations in the drifting frame: the aligned word of this lane's
-// column (bits m..31 of this lane, 0..m-1 of the right lane)
-__device__ __forceinline__ uint32_t drift_realign(uint32_t v, int m) {
-    const uint32_t r = bperm((((int)__lane_id() + 1) & 63) << 2, v);
-    if (m == 0) return v;
-    return m >= 32 ? r : __builtin_amdgcn_alignbit(r, v, (uint32_t)m);
-}
 
-// BYTE encoding through the same tiles: a lane's word column is 32 byte cells
-// (two 16-B loads per row), packed into one word on load (v_dot4_u32_u8
-// weights 1..128 per byte pair) and unpacked on store (nibble x 0x204081).
-__device__ __forceinline__ uint32_t pack32(uint4 lo, uint4 hi) {
-    constexpr uint32_t W0 = 0x08040201u, W1 = 0x80402010u;  // bit weights of cells 0-3 / 4-7
-    const uint32_t b3 = __builtin_amdgcn_udot4(hi.z, W0, __builtin_amdgcn_udot4(hi.w, W1, 0u, false), false);
-    const uint32_t b2 = __builtin_amdgcn_udot4(hi.x, W0, __builtin_amdgcn_udot4(hi.y, W1, b3 << 8, false), false);
-    const uint32_t b1 = __builtin_amdgcn_udot4(lo.z, W0, __builtin_amdgcn_udot4(lo.w, W1, b2 << 8, false), false);
-    return __builtin_amdgcn_udot4(lo.x, W0, __builtin_amdgcn_udot4(lo.y, W1, b1 << 8, false), false);
-}
-__device__ __forceinline__ uint32_t unpack_nibble(uint32_t w, int k) {
-    // cells 4k..4k+3 -> bytes 0..3 (bit j of the nibble lands on bit 8j)
-    return __umul24(__builtin_amdgcn_ubfe(w, 4 * k, 4), 0x204081u) & 0x01010101u;
-}
-
+// tstep_kernel: one workgroup owns a tile of 62 word columns x T owned rows.
+// Its kStackWaves waves are stacked vertically: wave i holds window rows
+// [i*R, (i+1)*R) of a (kStackWaves*R)-row window that starts K rows above the
+// tile (T = kStackWaves*R - 2K), one 32-cell word per lane and register row
+// (lane l holds word column 62*tx + l - 1; lanes 0 and 63 are the one-word
+// x-apron of the tile).  Each generation a wave publishes the horizontal sums
+// of its first and last row in LDS, one barrier, and takes its neighbours'
+// (the only values that cross waves); the window's own top/bottom K rows and
+// the edge lanes absorb the wrong values that enter from outside (K rows / K
+// <= 32 bits after K generations), so rows [K, K+T) of lanes 1..62 are exact.
+// Bit: centred frame (bit_hsum); byte: drifting frame (bit_hsum_drift; +2 %
+// there, -1 % for bit: profiles/r01/drift_ab.jsonl).
 template <bool BYTE, int R, int K, bool WRAPX, bool WRAPY>
 __global__ __launch_bounds__(64 * kStackWaves, 4) void tstep_kernel(TArgs a) {  // 4 waves/SIMD: 2 tiles per CU
     static_assert(R >= 3 && K >= 1 && K <= 32, "window");
     constexpr int NW = kStackWaves;
     constexpr int T = NW * R - 2 * K;
     __shared__ uint32_t xch[2][NW][4][64];  // [parity][wave][top s0/s1, bottom s0/s1][lane]
-    constexpr bool DRIFT = kDrift[BYTE ? 1 : 0];
+    constexpr bool DRIFT = BYTE;
     const int lane = threadIdx.x & 63;
+    const int laddr = ((lane - 1) & 63) << 2;
     // wave index: uniform, so every row address below is scalar (SALU) math
     const int wi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#if LIFE_HSUM_MODE == 3
-    __shared__ uint32_t rowx[NW][66];  // per-wave neighbour row, zero pads at 0 and 65
-    uint32_t *slot = rowx[wi];
-    if (lane < 2) slot[lane * 65] = 0u;
-#else
-    uint32_t *slot = nullptr;
-#endif
     const int64_t nwg = a.first[a.nreg];
     if ((int64_t)blockIdx.x >= nwg) return;  // whole workgroup
-#if LIFE_XCD_ORDER
-    // XCD-aware order (build-time switch, off: bit unchanged, byte -11 %,
-    // profiles/r01/xcd_order.txt): the dispatcher deals workgroups round-robin over the 8
-    // XCDs; give each XCD a contiguous run of tiles, walked down tile columns,
-    // so the 2K ghost rows a tile shares with the one below it are re-read
-    // from that XCD's L2 (bijective for any nwg).
-    const int64_t b = blockIdx.x, x = b % 8, per = nwg / 8, rem = nwg % 8;
-    const int64_t wg = (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + b / 8;
-#else
     const int64_t wg = blockIdx.x;
-#endif
     int k = 0;
     while (k + 1 < a.nreg && wg >= a.first[k + 1]) ++k;
     const int64_t wr = wg - a.first[k];
-#if LIFE_XCD_ORDER
-    const int64_t nty = a.ty1[k] - a.ty0[k];
-    const int64_t ty = a.ty0[k] + wr % nty, tx = a.tx0[k] + wr / nty;
-#else
     const int64_t ntx = a.tx1[k] - a.tx0[k];
     const int64_t tx = a.tx0[k] + wr % ntx, ty = a.ty0[k] + wr / ntx;
-#endif
     const int64_t j = tx * 62 + lane - 1;  // word column of this lane
     int64_t jl;
     if (WRAPX) {
@@ -515,22 +342,26 @@ __global__ __launch_bounds__(64 * kStackWaves, 4) void tstep_kernel(TArgs a) {  
             v[r] = *reinterpret_cast<const uint32_t *>(p + voff);
         }
         ++y;
-        if (WRAPY) {
-            if (y == a.h) {
-                y = 0;
-                p = row0;
-            } else {
-                p += a.pitch;
-            }
+        if (WRAPY && y == a.h) {
+            y = 0;
+            p = row0;
         } else {
             p += a.pitch;
         }
     }
+    auto hsum = [&](uint32_t x, uint32_t &s0, uint32_t &s1, uint32_t &L) {
+        if (DRIFT) {
+            bit_hsum_drift(x, laddr, s0, s1, L);
+        } else {
+            bit_hsum(x, s0, s1);
+            L = x;
+        }
+    };
     for (int g = 0; g < a.m; ++g) {
         const int par = g & 1;
         uint32_t t0, t1, b0, b1, tL, bL;  // xL: the row's own cells in the frame used
-        hsum_any<DRIFT>(v[0], t0, t1, tL, slot);
-        hsum_any<DRIFT>(v[R - 1], b0, b1, bL, slot);
+        hsum(v[0], t0, t1, tL);
+        hsum(v[R - 1], b0, b1, bL);
         xch[par][wi][0][lane] = t0;
         xch[par][wi][1][lane] = t1;
         xch[par][wi][2][lane] = b0;
@@ -549,7 +380,7 @@ __global__ __launch_bounds__(64 * kStackWaves, 4) void tstep_kernel(TArgs a) {  
         // rows 1 .. R-2 need only this wave's rows: they run while the LDS
         // reads are in flight
         uint32_t p0 = t0, p1 = t1, c0, c1, cL;
-        hsum_any<DRIFT>(v[1], c0, c1, cL, slot);
+        hsum(v[1], c0, c1, cL);
         const uint32_t h10 = c0, h11 = c1;
 #pragma unroll
         for (int r = 1; r < R - 1; ++r) {
@@ -559,7 +390,7 @@ __global__ __launch_bounds__(64 * kStackWaves, 4) void tstep_kernel(TArgs a) {  
                 n1 = b1;
                 nL = bL;
             } else {
-                hsum_any<DRIFT>(v[r + 1], n0, n1, nL, slot);
+                hsum(v[r + 1], n0, n1, nL);
             }
             v[r] = BitEnc::rule1(p0, p1, c0, c1, n0, n1, cL);
             cL = nL;
@@ -582,179 +413,13 @@ __global__ __launch_bounds__(64 * kStackWaves, 4) void tstep_kernel(TArgs a) {  
         if (st && y0 + r < a.h) {
             if (BYTE) {
                 uint4 *o = reinterpret_cast<uint4 *>(q);
-                o[0] = make_uint4(unpack_nibble(v[r], 0), unpack_nibble(v[r], 1), unpack_nibble(v[r], 2),
-                                  unpack_nibble(v[r], 3));
-                o[1] = make_uint4(unpack_nibble(v[r], 4), unpack_nibble(v[r], 5), unpack_nibble(v[r], 6),
-                                  unpack_nibble(v[r], 7));
+                o[0] = unpack_half(v[r], 0);
+                o[1] = unpack_half(v[r], 1);
             } else {
                 *reinterpret_cast<uint32_t *>(q) = v[r];
             }
         }
         q += a.pitch;
-    }
-}
-
-// Chained temporal tiles: one workgroup walks a SEGMENT of a tile column top
-// to bottom, one K-generation window after the other, and hands each
-// window's last exact row down to the next window through LDS.  The same 8
-// stacked waves and per-generation barrier as tstep_kernel; what changes:
-// the horizontal sums of window row 8R-K-1 (exact for every generation the
-// launch runs) are kept per generation in `hist`, and the next window, which
-// starts right below them, takes them as the row above its top row instead of
-// zeros.  Its top rows stay exact, so a fed window stores 8R-K rows instead
-// of 8R-2K (bit R = 48: 352 instead of 320 of 384 rows computed), and one
-// launch is one round of ~2 workgroups per CU (segments sized to the CU count)
-// instead of ~14 rounds of tiles with a partial last round.
-struct CArgs {
-    const uint8_t *in;
-    uint8_t *out;
-    int64_t pitch, xoff, W, h, ya;
-    int64_t tx0, ncols;     // tile columns [tx0, tx0 + ncols)
-    int64_t yb, ye, seg;    // owned rows [yb, ye) in segments of `seg` rows
-    int32_t m;
-};
-
-template <bool BYTE, int R, int K, bool WRAPX, bool WRAPY>
-__global__ __launch_bounds__(64 * kStackWaves, 6) void tchain_kernel(CArgs a) {  // 6 waves/SIMD: 3 windows per CU, as tstep_kernel reaches
-    static_assert(R >= 3 && K >= 1 && K <= 32 && kStackWaves * R - K - 1 >= 0, "window");
-    constexpr int NW = kStackWaves;
-    constexpr int HW = (NW * R - K - 1) / R, HR = (NW * R - K - 1) % R;  // the handed-down row
-    __shared__ uint32_t xch[2][NW][4][64];
-    __shared__ uint32_t hist[2][K][2][64];  // [window parity][generation][s0/s1][lane]
-    __shared__ uint32_t junk[NW][2][64];     // where the other waves' copies of that row go
-    const int lane = threadIdx.x & 63;
-    const int wi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#if LIFE_HSUM_MODE == 3
-    __shared__ uint32_t rowx[NW][66];
-    uint32_t *slot = rowx[wi];
-    if (lane < 2) slot[lane * 65] = 0u;
-#else
-    uint32_t *slot = nullptr;
-#endif
-    const int64_t tx = a.tx0 + (int64_t)blockIdx.x % a.ncols;
-    const int64_t s0 = a.yb + (int64_t)(blockIdx.x / a.ncols) * a.seg;
-    const int64_t s1 = s0 + a.seg < a.ye ? s0 + a.seg : a.ye;
-    if (s0 >= s1) return;  // whole workgroup
-    const int64_t j = tx * 62 + lane - 1;
-    int64_t jl;
-    if (WRAPX) {
-        jl = j % a.W;
-        if (jl < 0) jl += a.W;
-    } else {
-        jl = j > a.W ? a.W : j;
-    }
-    const uint32_t voff = (uint32_t)(a.xoff + (BYTE ? 32 : 4) * jl);
-    const bool st = lane >= 1 && lane <= 62 && j < a.W;
-    const uint8_t *row0 = a.in + a.ya * a.pitch;
-    int64_t top = s0 - K;  // window top (owned row of wave 0's register row 0)
-    for (int win = 0;; ++win) {
-        const bool fed = win > 0;
-        const int hp = win & 1;
-        // Every wave stores its copy of register row HR each generation (no
-        // branch inside the unrolled row loop: that split costs ~27 VGPRs);
-        // only wave HW's lands in hist.
-        uint32_t *const hdst = wi == HW ? &hist[hp ^ 1][0][0][0] : &junk[wi][0][0];
-        const int hstride = wi == HW ? 128 : 0;
-        const int64_t y0 = top + (int64_t)wi * R;
-        int64_t y = y0;
-        if (WRAPY) {
-            y %= a.h;
-            if (y < 0) y += a.h;
-        }
-        const uint8_t *p = row0 + y * a.pitch;
-        uint32_t v[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            if (BYTE) {
-                const uint4 *q = reinterpret_cast<const uint4 *>(p + voff);
-                v[r] = pack32(q[0], q[1]);
-            } else {
-                v[r] = *reinterpret_cast<const uint32_t *>(p + voff);
-            }
-            ++y;
-            if (WRAPY && y == a.h) {
-                y = 0;
-                p = row0;
-            } else {
-                p += a.pitch;
-            }
-        }
-        for (int g = 0; g < a.m; ++g) {
-            const int par = g & 1;
-            uint32_t t0, t1, b0, b1;
-            bit_hsum(v[0], t0, t1, slot);
-            bit_hsum(v[R - 1], b0, b1, slot);
-            xch[par][wi][0][lane] = t0;
-            xch[par][wi][1][lane] = t1;
-            xch[par][wi][2][lane] = b0;
-            xch[par][wi][3][lane] = b1;
-            if (HR == 0 || HR == R - 1) {
-                hdst[g * hstride + lane] = HR == 0 ? t0 : b0;
-                hdst[g * hstride + 64 + lane] = HR == 0 ? t1 : b1;
-            }
-            __syncthreads();
-            uint32_t a0 = 0u, a1 = 0u, d0 = 0u, d1 = 0u;
-            if (wi > 0) {
-                a0 = xch[par][wi - 1][2][lane];
-                a1 = xch[par][wi - 1][3][lane];
-            } else if (fed) {  // the previous window's row above this one
-                a0 = hist[hp][g][0][lane];
-                a1 = hist[hp][g][1][lane];
-            }
-            if (wi < NW - 1) {
-                d0 = xch[par][wi + 1][0][lane];
-                d1 = xch[par][wi + 1][1][lane];
-            }
-            uint32_t p0 = t0, p1 = t1, c0, c1;
-            bit_hsum(v[1], c0, c1, slot);
-            if (HR == 1) {
-                hdst[g * hstride + lane] = c0;
-                hdst[g * hstride + 64 + lane] = c1;
-            }
-            const uint32_t h10 = c0, h11 = c1;
-#pragma unroll
-            for (int r = 1; r < R - 1; ++r) {
-                uint32_t n0, n1;
-                if (r + 1 == R - 1) {
-                    n0 = b0;
-                    n1 = b1;
-                } else {
-                    bit_hsum(v[r + 1], n0, n1, slot);
-                    if (r + 1 == HR && HR > 1) {
-                        hdst[g * hstride + lane] = n0;
-                        hdst[g * hstride + 64 + lane] = n1;
-                    }
-                }
-                v[r] = BitEnc::rule1(p0, p1, c0, c1, n0, n1, v[r]);
-                p0 = c0;
-                p1 = c1;
-                c0 = n0;
-                c1 = n1;
-            }
-            v[R - 1] = BitEnc::rule1(p0, p1, b0, b1, d0, d1, v[R - 1]);
-            v[0] = BitEnc::rule1(a0, a1, t0, t1, h10, h11, v[0]);
-        }
-        // exact rows: [top + (fed ? 0 : K), top + NW*R - K), clipped to the segment
-        const int64_t lo = fed ? top : s0, hi0 = top + NW * R - K, hi = hi0 < s1 ? hi0 : s1;
-        uint8_t *q = a.out + (a.ya + y0) * a.pitch + voff;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int64_t yy = y0 + r;
-            if (st && yy >= lo && yy < hi && yy < a.h) {
-                if (BYTE) {
-                    uint4 *o = reinterpret_cast<uint4 *>(q);
-                    o[0] = make_uint4(unpack_nibble(v[r], 0), unpack_nibble(v[r], 1), unpack_nibble(v[r], 2),
-                                      unpack_nibble(v[r], 3));
-                    o[1] = make_uint4(unpack_nibble(v[r], 4), unpack_nibble(v[r], 5), unpack_nibble(v[r], 6),
-                                      unpack_nibble(v[r], 7));
-                } else {
-                    *reinterpret_cast<uint32_t *>(q) = v[r];
-                }
-            }
-            q += a.pitch;
-        }
-        if (hi >= s1) break;  // uniform: every wave leaves after the same window
-        top = hi0;
     }
 }
 
@@ -1326,14 +991,12 @@ int temporal_rows(bool bit) {
     return temporal_rows_ok(nr) ? nr : (bit ? 48 : 32);
 }
 
-// Per register row and generation: bit_hsum = 2 neighbour fetches (DPP on
-// the VALU or ds_bpermute on the LDS pipe, LIFE_HSUM_MODE) + 2 v_alignbit +
-// 2 v_bitop3, rule1 = 8 v_bitop3; kStackWaves waves of temporal_rows() rows
-// per tile; the byte encoding adds pack (8 v_dot4 + 3 shifts) and unpack
-// (8 x bfe/mul24/and) once per row and launch.
-constexpr double kValuPerRow = LIFE_HSUM_MODE == 0 ? 14.0 : LIFE_HSUM_MODE == 1 ? 12.0 : 13.0;
+// Per register row and generation: bit_hsum = 1 DPP move + 2 v_alignbit + 2
+// v_bitop3 (+ 1 ds_bpermute on the LDS pipe), rule1 = 8 v_bitop3: 13; the
+// byte tiles run the drifting frame (12) and add pack (8 v_dot4 + 3 shifts)
+// and unpack (8 x bfe/mul24/and) once per row and launch.
 double tstep_valu_per_tile_lane(int m, bool byte) {
-    const double per_row = kDrift[byte ? 1 : 0] ? 12.0 : kValuPerRow;  // drifting frame: 12
+    const double per_row = byte ? 12.0 : 13.0;
     return (double)kStackWaves * (double)temporal_rows(!byte) * (per_row * (double)m + (byte ? 35.0 : 0.0));
 }
 
@@ -1432,101 +1095,6 @@ hipError_t launch_k(const TArgs &a, Wrap wrap, unsigned grid, hipStream_t s) {
     }
 }
 }  // namespace
-
-namespace {
-template <bool BYTE, int R>
-hipError_t launch_c(const CArgs &a, Wrap wrap, unsigned grid, hipStream_t s) {
-    constexpr unsigned kThreads = 64 * kStackWaves;
-    if (wrap.x && wrap.y)
-        tchain_kernel<BYTE, R, 32, true, true><<<grid, kThreads, 0, s>>>(a);
-    else if (wrap.x)
-        tchain_kernel<BYTE, R, 32, true, false><<<grid, kThreads, 0, s>>>(a);
-    else if (wrap.y)
-        tchain_kernel<BYTE, R, 32, false, true><<<grid, kThreads, 0, s>>>(a);
-    else
-        tchain_kernel<BYTE, R, 32, false, false><<<grid, kThreads, 0, s>>>(a);
-    return hipGetLastError();
-}
-
-int device_cus() {
-    static int cus[64] = {0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (!cus[dev]) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-        cus[dev] = n;
-    }
-    return cus[dev];
-}
-}  // namespace
-
-bool chain_supported(const life_layout &L) {
-    const int R = temporal_rows(is_bit(L));
-    return L.generations_per_exchange == 32 && (R == 32 || R == 48);
-}
-
-// Resident chained workgroups per CU of the instance a layout runs
-// (hipOccupancy: 3 for both encodings -- 6 waves per SIMD, 52 KiB of LDS each).
-template <bool BYTE, int R>
-int chain_per_cu() {
-    static const int n = [] {
-        int v = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, tchain_kernel<BYTE, R, 32, true, true>,
-                                                         64 * kStackWaves, 0) != hipSuccess || v <= 0)
-            v = 2;
-        return v;
-    }();
-    return n;
-}
-
-int chain_slots(const life_layout &L, int reserve) {
-    static const int env = [] {
-        const char *e = getenv("LIFE_CHAIN_SLOTS");
-        return e ? atoi(e) : 0;
-    }();
-    const bool bit = is_bit(L);
-    const int R = temporal_rows(bit);
-    const int per_cu = bit ? (R == 48 ? chain_per_cu<false, 48>() : chain_per_cu<false, 32>())
-                           : (R == 48 ? chain_per_cu<true, 48>() : chain_per_cu<true, 32>());
-    const int slots = env > 0 ? env : per_cu * device_cus();
-    return slots - reserve > 1 ? slots - reserve : 1;
-}
-
-hipError_t launch_tchain(const life_layout &L, const uint8_t *in, uint8_t *out, int64_t tx0, int64_t tx1,
-                         int64_t yb, int64_t ye, int m, Wrap wrap, int slots, hipStream_t s, double *windows) {
-    if (windows) *windows = 0.0;
-    if (!chain_supported(L) || m <= 0 || m > 32 || L.yapron != 32 || slots < 1) return hipErrorInvalidValue;
-    if (tx1 <= tx0 || ye <= yb) return hipSuccess;
-    const int64_t R = temporal_rows(is_bit(L)), K = 32;
-    const int64_t T1 = kStackWaves * R - 2 * K, T2 = kStackWaves * R - K;  // rows of a first / fed window
-    const int64_t rows = ye - yb, ncols = tx1 - tx0;
-    const int64_t nseg_max = slots / ncols > 1 ? slots / ncols : 1;
-    const int64_t per = (rows + nseg_max - 1) / nseg_max;
-    const int64_t nt = per <= T1 ? 1 : 1 + (per - T1 + T2 - 1) / T2;  // windows per full segment
-    const int64_t seg = T1 + (nt - 1) * T2;
-    const int64_t nseg = (rows + seg - 1) / seg;
-    const int64_t last = rows - (nseg - 1) * seg;
-    const int64_t nt_last = last <= T1 ? 1 : 1 + (last - T1 + T2 - 1) / T2;
-    if (windows) *windows = (double)ncols * (double)((nseg - 1) * nt + nt_last);
-    CArgs a;
-    a.in = in;
-    a.out = out;
-    a.pitch = L.pitch;
-    a.xoff = L.xoff;
-    a.W = (L.w + 31) / 32;
-    a.h = L.h;
-    a.ya = L.yapron;
-    a.tx0 = tx0;
-    a.ncols = ncols;
-    a.yb = yb;
-    a.ye = ye;
-    a.seg = seg;
-    a.m = m;
-    const unsigned grid = (unsigned)(ncols * nseg);
-    if (is_bit(L)) return R == 48 ? launch_c<false, 48>(a, wrap, grid, s) : launch_c<false, 32>(a, wrap, grid, s);
-    return R == 48 ? launch_c<true, 48>(a, wrap, grid, s) : launch_c<true, 32>(a, wrap, grid, s);
-}
 
 TileGeom tile_geom(const life_layout &L) {
     TileGeom g;

@@ -57,15 +57,15 @@ int life_dims_choose(int64_t nx, int64_t ny, int n, int policy, int dims[2]) {
 }
 
 // Generations per halo exchange of the temporally blocked layout, per
-// encoding: LIFE_TEMPORAL_DEPTH (bit) / LIFE_TEMPORAL_DEPTH_BYTE, or 16 / 24
-// / 32 from the environment variables of the same names (read once; every rank
+// encoding: LIFE_TEMPORAL_DEPTH (bit) / LIFE_TEMPORAL_DEPTH_BYTE, or 8 / 12 /
+// 16 / 24 / 32 from the environment variables of the same names (read once; every rank
 // of a job must see the same values); 1 selects the one-generation layouts
 // (a measurement knob: the HBM-bound kernels).  The byte encoding moves 8x
 // the bytes per cell, so it amortises each HBM pass over more generations.
 static int env_depth(const char *name, int dflt) {
     const char *e = getenv(name);
     const int v = e ? atoi(e) : 0;
-    return v == 1 || v == 16 || v == 24 || v == 32 ? v : dflt;
+    return v == 1 || v == 8 || v == 12 || v == 16 || v == 24 || v == 32 ? v : dflt;
 }
 static int temporal_depth(int kernel) {
     static const int kbit = env_depth("LIFE_TEMPORAL_DEPTH", LIFE_TEMPORAL_DEPTH);

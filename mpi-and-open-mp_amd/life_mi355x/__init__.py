@@ -39,9 +39,9 @@ KERNELS = {"byte": KERNEL_BYTE, "bit": KERNEL_BIT}
 XPORT_AUTO, XPORT_RCCL, XPORT_LOCAL = 0, 1, 2
 HALO_SEND, HALO_RECV, HALO_FILL = 0, 1, 2
 HALO_COLUMN, HALO_ROW = 0, 1
-OPT_SMALL_GRID, OPT_OVERLAP, OPT_CHAIN, OPT_SMALL_WINDOW = 1, 2, 3, 4
+OPT_SMALL_GRID, OPT_OVERLAP, OPT_SWEEP, OPT_SMALL_WINDOW = 1, 2, 3, 4
 # LIFE_TEMPORAL_DEPTH(_BYTE): generations per halo exchange of the temporal layouts
-TEMPORAL_DEPTH = {"bit": 32, "byte": 32}
+TEMPORAL_DEPTH = {"bit": 16, "byte": 32}
 TEMPORAL_ROWS = {"bit": 48, "byte": 32}  # default register rows per wave of the temporal tiles
 
 # Every symbol include/life_mi355x.h declares (checked by tests/test_abi.py).
@@ -224,7 +224,7 @@ class Life:
     """
 
     def __init__(self, nx: int, ny: int, shards: int = 1, kernel="bit", dims=(0, 0),
-                 transport: int = XPORT_AUTO, small_grid: bool = True, overlap: bool = True, chain=None,
+                 transport: int = XPORT_AUTO, small_grid: bool = True, overlap: bool = True, sweep=None,
                  window=None, _handle=None):
         self.nx, self.ny = int(nx), int(ny)
         self.kernel = kernel_id(kernel)
@@ -247,11 +247,10 @@ class Life:
             self.configure(OPT_SMALL_WINDOW, int(window[0]) * 256 + int(window[1]))
         if not overlap:
             self.configure(OPT_OVERLAP, 0)
-        # chain: None (library default: independent tiles), True (chained
-        # temporal tiles), False, or an int > 1 = workgroups per chained launch
-        # (long chains on small grids)
-        if chain is not None:
-            self.configure(OPT_CHAIN, int(chain))
+        # sweep: None (library default: the tiled temporal stencil), True (the
+        # sweep stencil), or False
+        if sweep is not None:
+            self.configure(OPT_SWEEP, int(bool(sweep)))
 
     def configure(self, option: int, value: int) -> None:
         _check(_lib().life_dev_configure(self._h, option, value), "configure")

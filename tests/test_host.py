@@ -155,27 +155,25 @@ def test_halo_plan_is_symmetric(lm, kernel, nx, ny, dims):
                     assert (o[4], s_[4]) in ((0, lay[peer].h), (lay[r].h + ya, ya))
 
 
-@pytest.mark.parametrize("nx,ny,dims,temporal", [(65536, 65536, (1, 1), True), (262144, 131072, (4, 2), True),
-                                                 (1000, 37, (1, 1), True), (31, 37, (1, 1), False),
-                                                 (64, 7, (2, 1), True), (500, 500, (2, 1), True),
-                                                 (63, 9, (2, 1), False), (100, 64, (3, 2), True),
-                                                 (64, 14, (1, 2), False), (96, 64, (3, 2), True),
-                                                 (96, 62, (3, 2), False)])
-def test_temporal_mode_selection(lm, nx, ny, dims, temporal):
+@pytest.mark.parametrize("nx,ny,dims,wide", [(65536, 65536, (1, 1), True), (262144, 131072, (4, 2), True),
+                                             (1000, 37, (1, 1), True), (31, 37, (1, 1), False),
+                                             (64, 7, (2, 1), True), (500, 500, (2, 1), True),
+                                             (63, 9, (2, 1), False), (100, 64, (3, 2), True),
+                                             (64, 14, (1, 2), True), (96, 64, (3, 2), True),
+                                             (96, 62, (3, 2), True), (96, 30, (3, 2), True)])
+def test_temporal_mode_selection(lm, nx, ny, dims, wide):
     """Temporal blocking needs blocks >= 32 cells wide (any width: the right
-    column and apron may straddle words) and, on a partitioned y axis, >= K rows."""
+    column and apron may straddle words) and, on a partitioned y axis, >= K
+    rows (K = 16 bit, 32 byte)."""
     for r in range(dims[0] * dims[1]):
-        L = lm.layout_query(nx, ny, dims, r, "bit")
-        K = lm.TEMPORAL_DEPTH["bit"]
-        assert (L.generations_per_exchange == K) == temporal
-        assert (L.xapron, L.yapron) == ((32, K) if temporal else (1, 1))
-        assert L.rows == L.h + 2 * L.yapron
-        B = lm.layout_query(nx, ny, dims, r, "byte")  # the byte encoding takes the same tiles, K = 32
-        KB = lm.TEMPORAL_DEPTH["byte"]
-        tb = temporal and (dims[1] == 1 or ny // dims[1] >= KB)
-        assert (B.xapron, B.yapron, B.generations_per_exchange) == ((32, KB, KB) if tb else (1, 1, 1))
-        if tb:  # room for the 32-byte right apron and the whole 32-byte word holding its last cell
-            assert B.pitch >= B.xoff + 32 * ((B.w + 31) // 32 + 1)
+        for kernel in ("bit", "byte"):
+            L = lm.layout_query(nx, ny, dims, r, kernel)
+            K = lm.TEMPORAL_DEPTH[kernel]
+            t = wide and (dims[1] == 1 or ny // dims[1] >= K)
+            assert (L.xapron, L.yapron, L.generations_per_exchange) == ((32, K, K) if t else (1, 1, 1))
+            assert L.rows == L.h + 2 * L.yapron
+            if t and kernel == "byte":  # room for the 32-byte right apron and the whole 32-byte word holding its last cell
+                assert L.pitch >= L.xoff + 32 * ((L.w + 31) // 32 + 1)
 
 
 def test_bits_frame_roundtrip(lm, oracle, tmp_path):
