@@ -4,25 +4,31 @@
 A "step" is one generation (halo exchange + B3/S23 update) over the whole
 grid.  Default workload (BASELINE.json configs[4], weak scaling): a random
 50%-density 65536 x 65536 block per GPU, global grid
-(65536*dims0) x (65536*dims1) (dims: --partition below); N = 1 is the
-65536^2 single-GPU configuration the 80%-of-HBM-roofline target is quoted on.
-Inputs are generated on the device (counter-based splitmix64, the same
-generator as oracle/life_oracle.c) and are resident in HBM before timing.
+(65536*dims0) x (65536*dims1); N = 1 is the 65536^2 single-GPU configuration
+the 80%-of-HBM-roofline target is quoted on.  --scaling strong is configs[3]:
+one 65536^2 grid split over the N GPUs (2-D Cartesian blocks by default, as
+life_cart.c:117-124).  Inputs are generated on the device (counter-based
+splitmix64, the same generator as oracle/life_oracle.c) and are resident in
+HBM before timing.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--kernel bit|byte]
-                  [--size 65536] [--workload weak|p46gun_big]
-                  [--partition auto|cart|rows|cols]
+                  [--scaling weak|strong] [--size 65536]
+                  [--workload random|p46gun_big] [--partition auto|cart|rows|cols]
 
-Partition (life_dims_choose): "auto" (default) cuts the global grid into
-row strips, dims {1, N} (the 1-D decomposition of 3-life/5-gather), because
-measured per-GPU cost is 0-6 % lower than for 2-D blocks and every halo
-message is contiguous; "cart" is 6-cartesian's MPI_Dims_create {2,1} /
-{2,2} / {4,2}.  Either way each GPU owns one size x size block.
+Partition (life_dims_choose): "auto" (weak default) cuts the global grid into
+row strips, dims {1, N} (the 1-D decomposition of 3-life/5-gather): per-GPU
+cost measured 0-6 % lower than 2-D blocks and every halo message contiguous;
+"cart" (strong default) is 6-cartesian's MPI_Dims_create {2,1} / {2,2} / {4,2}.
 
 N > 1 runs one process per GPU under torch.distributed.run: torch.distributed
 (gloo) carries the bootstrap (RCCL unique id), the barriers and the
 max-over-ranks timing; the halo data path is RCCL ncclSend/ncclRecv issued by
-liblife_mi355x.so itself.
+liblife_mi355x.so itself.  `--gpus N` without a launcher drives N shards from
+one process (one per GPU, ncclCommInitAll; or, with fewer GPUs than shards,
+device-local copies -- how a 1-GPU box rehearses the partitioned schedule).
+Every N > 1 line ends with "phases" (mean ring / interior / halo / block
+times per exchange, from HIP events on the three streams) and
+"parity_vs_1gpu" (the N-shard grid against the same grid run as one shard).
 """
 from __future__ import annotations
 
@@ -56,22 +62,30 @@ VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    # defaults: whole multiples of the temporal kernel's 32 generations per
-    # launch; one untimed launch, then generations 32..1024 of the random soup
-    # (configs[2]/[4] run 1000 generations from the random start).  Launches
-    # get faster as the soup thins out (65536^2 bit: 1.61 ms per launch at
-    # the start, 1.36 ms after ~10 launches, profiles/r01/bench_warmup.jsonl);
-    # timing the whole run, not only its cooled tail, keeps both in the rate.
+    # defaults: one untimed launch, then generations 32..1024 of the random
+    # soup (configs[2]/[4] run 1000 generations from the random start; a
+    # multiple of both temporal depths, 16 and 32).  Launches get faster as the
+    # soup thins out (profiles/r01/bench_warmup.jsonl); timing the whole run,
+    # not only its cooled tail, keeps both in the rate.
     p.add_argument("--steps", type=int, default=992)
     p.add_argument("--warmup", type=int, default=32)
     p.add_argument("--kernel", default="bit", choices=["bit", "byte"])
-    p.add_argument("--size", type=int, default=65536, help="per-GPU block edge (weak scaling)")
-    p.add_argument("--workload", default="weak", choices=["weak", "p46gun_big"])
-    p.add_argument("--partition", default="auto", choices=["auto", "cart", "rows", "cols"],
-                   help="shard shape (life_dims_choose): auto = row strips when each is >= 1024 rows tall")
+    p.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                   help="weak: a size^2 block per GPU (configs[4]); strong: one size^2 grid split over the GPUs "
+                        "(configs[3])")
+    p.add_argument("--size", type=int, default=65536,
+                   help="block edge per GPU (weak) or global grid edge (strong)")
+    p.add_argument("--workload", default="random", choices=["random", "p46gun_big"])
+    p.add_argument("--partition", default=None, choices=["auto", "cart", "rows", "cols"],
+                   help="shard shape (life_dims_choose); default: cart (MPI_Dims_create, life_cart.c:117-118) "
+                        "for strong scaling, auto (row strips when each is >= 1024 rows tall) for weak")
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline sample budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--parity-seconds", type=float, default=60.0,
+                   help="N > 1: the 1-GPU reference re-runs the timed generations when that is estimated to take "
+                        "less than this, else a fresh 3K+1-generation run of both")
+    p.add_argument("--no-parity", action="store_true")
     p.add_argument("--temporal", default="tiles", choices=["sweep", "tiles"],
                    help="temporally blocked kernel: the tiled tstep_kernel (default) or sweep_kernel")
     p.add_argument("--rank-mode", action="store_true",
@@ -82,7 +96,9 @@ def parse():
 def cpu_baseline(target_s: float):
     """The CPU oracle (a restatement of the reference's row-strip life_step,
     3-life/life_mpi.c:150-176, one OpenMP thread per strip) on a bounded
-    sample of the same workload: a random 50% 4096^2 grid."""
+    sample of the same workload: a random 50% 4096^2 grid.  The reference's
+    own mpirun rates were measured in the build container (the reference
+    never travels to the GPU box) and are reported beside it as constants."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
@@ -96,25 +112,19 @@ def cpu_baseline(target_s: float):
     t = time.perf_counter()
     O.life_run(g, gens, threads)
     dt = time.perf_counter() - t
-    res = {"value": n * n * gens / dt / 1e9, "unit": "Gcell-updates/s", "cores": threads, "kind": "port",
-           "sample": f"random 50% {n}x{n}, {gens} generations, oracle/life_oracle.c OpenMP row strips, "
-                     f"{dt:.1f} s"}
-    ref = O.ref_lib()
-    if ref is not None:  # the reference's own life_step (3-life/life2d.c), when built
-        m = 2048
-        g2 = O.fill_random(m, m, 12345, 0.5)
-        t = time.perf_counter()
-        O.ref_life_run(g2, 2)
-        dt2 = time.perf_counter() - t
-        res["reference_1core"] = {"value": m * m * 2 / dt2 / 1e9, "unit": "Gcell-updates/s",
-                                  "sample": f"random 50% {m}x{m}, 2 generations, reference life_step "
-                                            "(3-life/life2d.c:104-130, gcc -O2), 1 core"}
-    return res
+    return {"value": n * n * gens / dt / 1e9, "unit": "Gcell-updates/s", "cores": threads, "kind": "port",
+            "sample": f"random 50% {n}x{n}, {gens} generations, oracle/life_oracle.c OpenMP row strips "
+                      f"({threads} threads), {dt:.1f} s",
+            "reference_mpirun_container": {
+                "unit": "Gcell-updates/s", "cores": 8,
+                "life_cart_np8_p46gun_big": 0.622, "life_cart_np8_random4096_steady": 0.357,
+                "source": "BASELINE.md 'Re-measured in the survey container': reference 6-cartesian/life_cart.c, "
+                          "gcc -O2, MPICH 3.3.2, mpiexec -n 8 on the build container's 8-core Xeon (not this host)"}}
 
 
 def load_traffic(variant: str, size: int):
     """HBM bytes per stencil launch from the committed rocprofv3 PMC summary
-    (scripts/traffic_summary.py); None where the access width is uncalibrated."""
+    (scripts/traffic_summary.py); None where not measured for this variant."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as f:
@@ -122,6 +132,53 @@ def load_traffic(variant: str, size: int):
         return t.get(f"{variant}_{size}")
     except (OSError, ValueError):
         return None
+
+
+def make_life(a, nx, ny, dims, rank_mode, dist, rank, world, local_rank):
+    if rank_mode:
+        uid = [lm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        life = lm.Life.for_rank(nx, ny, rank, world, uid[0], local_rank, kernel=a.kernel, dims=dims)
+    else:
+        life = lm.Life(nx, ny, shards=a.gpus, kernel=a.kernel, dims=dims)
+    if a.temporal == "sweep":
+        life.configure(lm.OPT_SWEEP, 1)
+    return life
+
+
+def init_grid(life, a, grid):
+    if grid is not None:
+        life.upload(grid)
+    else:
+        life.fill_random(a.seed, 0.5)
+
+
+def parity_vs_1gpu(a, life, grid, nx, ny, gens_done, elapsed, n_gpus, rank, dist, barrier_sync):
+    """The N-shard result against the same grid and generations run as ONE
+    shard on GPU 0: the census checksum (sum of mix64(global index) over live
+    cells, partition- and encoding-independent) and the live count.  The
+    timed run's own end state is compared when re-running it on one GPU is
+    estimated to take under --parity-seconds; otherwise both sides run a fresh
+    3K+1 generations (several halo-exchange periods and a partial one)."""
+    K = life.layout().generations_per_exchange
+    same_run = elapsed * n_gpus * 1.3 < a.parity_seconds
+    gens = gens_done
+    if not same_run:
+        gens = 3 * K + 1
+        init_grid(life, a, grid)
+        life.step(gens)
+    got = (life.checksum(), life.live_count())  # collective in rank mode
+    want = None
+    if rank == 0:
+        with lm.Life(nx, ny, shards=1, kernel=a.kernel) as ref:
+            init_grid(ref, a, grid)
+            ref.step(gens)
+            want = (ref.checksum(), ref.live_count())
+    barrier_sync()
+    if rank != 0:
+        return None
+    return {"ok": got == want, "generations": gens, "same_run": same_run, "checksum": got[0], "live": got[1],
+            "reference": {"checksum": want[0], "live": want[1], "shards": 1, "device": 0}}
 
 
 def main():
@@ -136,31 +193,31 @@ def main():
 
         dist.init_process_group("gloo")
     n_gpus = world if world > 1 else a.gpus
+    strong = a.scaling == "strong"
+    partition = a.partition or ("cart" if strong else "auto")
+    grid = None
     if a.workload == "p46gun_big":
-        steps_cfg, _, grid = lm.load_cfg(os.path.join(ROOT, "tests", "golden", "cfg", "p46gun_big.cfg"))
+        _, _, grid = lm.load_cfg(os.path.join(ROOT, "tests", "golden", "cfg", "p46gun_big.cfg"))
         ny, nx = grid.shape
-        dims = lm.dims_choose(nx, ny, n_gpus, a.partition)
+        dims = lm.dims_choose(nx, ny, n_gpus, partition)
+        strong = True
         workload = "p46gun_big.cfg 500x500 (configs[1])"
+    elif strong:
+        nx = ny = a.size
+        dims = lm.dims_choose(nx, ny, n_gpus, partition)
+        workload = (f"random 50% {a.size}^2 global, {dims[0]}x{dims[1]} blocks over {n_gpus} GPU(s) "
+                    f"(configs[3] strong scaling)")
     else:
-        # weak scaling: the shape is chosen for n_gpus blocks of size^2 stacked as strips
-        dims = lm.dims_choose(a.size, a.size * n_gpus, n_gpus, a.partition)
+        # weak scaling: the shape is chosen for n_gpus blocks of size^2
+        dims = lm.dims_choose(a.size, a.size * n_gpus, n_gpus, partition)
         nx, ny = a.size * dims[0], a.size * dims[1]
-        grid = None
-        workload = f"random 50% {a.size}^2 per GPU, global {nx}x{ny} (configs[4] weak scaling)"
+        label = {32768: "configs[2]", 65536: "configs[4] weak scaling"}.get(a.size, "weak scaling")
+        if n_gpus == 1 and a.size == 65536:
+            label = "configs[4] at N=1 = the 65536^2 single-GPU roofline config"
+        workload = f"random 50% {a.size}^2 per GPU, global {nx}x{ny} ({label})"
 
-    if rank_mode:
-        uid = [lm.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        life = lm.Life.for_rank(nx, ny, rank, world, uid[0], local_rank, kernel=a.kernel, dims=dims)
-    else:
-        life = lm.Life(nx, ny, shards=a.gpus, kernel=a.kernel, dims=dims)
-    if a.temporal == "sweep":
-        life.configure(lm.OPT_SWEEP, 1)
-
-    if grid is not None:
-        life.upload(grid)
-    else:
-        life.fill_random(a.seed, 0.5)
+    life = make_life(a, nx, ny, dims, rank_mode, dist, rank, world, local_rank)
+    init_grid(life, a, grid)
     life.step(a.warmup)
     life.sync()
 
@@ -178,30 +235,69 @@ def main():
     life.step(a.steps)
     barrier_sync()
     elapsed = time.perf_counter() - t0
-    if dist is not None:
+
+    def allmax(vals):
+        if dist is None:
+            return vals
         import torch
 
-        t = torch.tensor([elapsed], dtype=torch.float64)
+        t = torch.tensor(vals, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        return [float(x) for x in t]
+
+    elapsed = allmax([elapsed])[0]
     avg_ms, launches, bytes_per_launch = life.kernel_stats()
     updates_per_launch, valu_per_launch = life.kernel_work()
+    ph = life.phase_stats()
+    exposed = allmax([ph["block_ms"] - ph["interior_ms"], ph["block_ms"], ph["halo_ms"]])
     live = life.live_count()
+    lay = life.layout()
+    temporal = lay.generations_per_exchange > 1
 
     # a measured stream-copy ceiling next to the spec peak
     # (rank 0's GPU, after the timed region; 2 x 2 GiB buffers)
     copy_gbps = lm.measure_copy(local_rank, 2 << 30, 5) if rank == 0 else 0.0
 
+    parity = None
+    if n_gpus > 1 and not a.no_parity:
+        parity = parity_vs_1gpu(a, life, grid, nx, ny, a.warmup + a.steps, elapsed, n_gpus, rank, dist,
+                                barrier_sync)
+
     if rank == 0:
         cells = float(nx) * float(ny) * a.steps
         bpu = 0.25 if a.kernel == "bit" else 2.0  # algorithmic HBM bytes per cell-update
         value = cells / elapsed / 1e9
-        achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-        gens_per_launch = updates_per_launch / (bytes_per_launch / (0.25 if a.kernel == "bit" else 2.0)) \
-            if bytes_per_launch > 0 else 0.0
-        temporal = life.layout().generations_per_exchange > 1
+        hbm = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        gens_per_launch = updates_per_launch / (bytes_per_launch / bpu) if bytes_per_launch > 0 else 0.0
         variant = a.kernel + ("_temporal" if temporal else "_onegen")
-        traffic = load_traffic(variant, a.size) if a.workload == "weak" else None
+        if temporal and a.temporal == "sweep":
+            variant += "_sweep"
+        traffic = load_traffic(variant, a.size) if (a.workload == "random" and not strong) else None
+        hbm_obj = {"achieved": round(hbm, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                   "frac": round(hbm / HBM_PEAK_GBS, 4),
+                   "bytes_per_launch": bytes_per_launch,
+                   "copy_ceiling_GBps": round(copy_gbps, 1),
+                   "frac_of_copy_ceiling": round(hbm / copy_gbps, 4) if copy_gbps > 0 else None,
+                   # SURVEY 8(d)'s per-update figure (0.25 B bit / 2 B byte) x the
+                   # cell-updates of a launch: above the HBM peak once a launch
+                   # advances K > 1 generations per pass over HBM
+                   "per_generation_equivalent_GBps": round(updates_per_launch * bpu / (avg_ms * 1e-3) / 1e9, 1)
+                   if avg_ms > 0 else 0.0}
+        tops = valu_per_launch / (avg_ms * 1e-3) / 1e12 if (valu_per_launch > 0 and avg_ms > 0) else 0.0
+        if temporal and tops > 0:
+            # the temporally blocked kernels are bound by VALU issue, not HBM:
+            # modelled lane-ops per launch (checked against SQ_INSTS_VALU) over
+            # the same mean launch time, against 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
+            roofline = {"bound": "valu", "achieved": round(tops, 2), "peak": round(VALU_PEAK_TOPS, 2),
+                        "unit": "Tlane-op/s", "frac": round(tops / VALU_PEAK_TOPS, 4), "traffic": traffic,
+                        "kernel_avg_ms": round(avg_ms, 5), "kernel_launches": launches,
+                        "generations_per_launch": round(gens_per_launch, 3), "ops_per_launch": valu_per_launch,
+                        "model": "per register row and generation 13 VALU (tiles; byte: 12 + pack/unpack) or "
+                                 "12 per stage-step (sweep), life_kernels.hip / life_sweep.hip",
+                        "hbm": hbm_obj}
+        else:
+            roofline = dict(hbm_obj, bound="hbm", traffic=traffic, kernel_avg_ms=round(avg_ms, 5),
+                            kernel_launches=launches, generations_per_launch=round(gens_per_launch, 3))
         out = {
             "metric": "Gcell-updates/sec at 1/2/4/8 MI355X + % of HBM roofline, bit-exact",
             "value": round(value, 3),
@@ -211,41 +307,30 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "u32 (1 bit/cell)" if a.kernel == "bit" else "u8 (1 byte/cell)",
             "data": "synthetic (device-side splitmix64 random, density 0.5)" if grid is None
                     else "p46gun_big.cfg pattern",
             "config": {"workload": workload, "nx": nx, "ny": ny, "dims": list(dims), "kernel": a.kernel,
-                       "parallelism": f"cartesian {dims[0]}x{dims[1]}", "partition": a.partition,
-                       "live_cells_end": live},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel_avg_ms": round(avg_ms, 5), "kernel_launches": launches,
-                         "bytes_per_launch": bytes_per_launch,
-                         "generations_per_launch": round(gens_per_launch, 3),
-                         # SURVEY 8(d)'s per-update figure (0.25 B bit / 2 B byte) x the
-                         # cell-updates of a launch: above the HBM peak once a launch
-                         # advances K > 1 generations per pass over HBM
-                         "per_generation_equivalent_GBps": round(
-                             updates_per_launch * (0.25 if a.kernel == "bit" else 2.0) / (avg_ms * 1e-3) / 1e9, 1)
-                         if avg_ms > 0 else 0.0,
-                         # the north-star question "% of HBM roofline" in cell-update terms: the
-                         # rate a one-generation-per-HBM-pass kernel would reach at the HBM peak on
-                         # n_gpus GPUs (8 TB/s / 0.25 B or 2 B per update), and value against it
-                         "copy_ceiling_GBps": round(copy_gbps, 1),
-                         "frac_of_copy_ceiling": round(achieved / copy_gbps, 4) if copy_gbps > 0 else None,
-                         "hbm_bound_cell_rate": round(n_gpus * HBM_PEAK_GBS / bpu, 1),
-                         "cell_rate_vs_hbm_bound": round(value / (n_gpus * HBM_PEAK_GBS / bpu), 4)},
+                       "parallelism": f"cartesian {dims[0]}x{dims[1]}"
+                                      + (" (one process per GPU, RCCL)" if rank_mode else
+                                         f" ({life.world()['nlocal']} shards in one process, "
+                                         f"{['auto', 'RCCL', 'LOCAL'][life.world()['transport']]} transport)"),
+                       "partition": partition, "temporal_kernel": a.temporal if temporal else "one-generation",
+                       "generations_per_exchange": lay.generations_per_exchange, "live_cells_end": live},
+            "roofline": roofline,
         }
-        if valu_per_launch > 0 and avg_ms > 0:
-            # the temporally blocked kernel is VALU-issue bound, not HBM bound
-            tops = valu_per_launch / (avg_ms * 1e-3) / 1e12
-            out["valu"] = {"bound": "valu", "achieved": round(tops, 2), "peak": round(VALU_PEAK_TOPS, 2),
-                           "unit": "Tlane-op/s", "frac": round(tops / VALU_PEAK_TOPS, 4),
-                           "ops_per_launch": valu_per_launch, "model": "13 VALU ops per register row "
-                           "and generation + byte pack/unpack (life_kernels.hip tstep_valu_per_tile_lane), "
-                           "within 2% of SQ_INSTS_VALU (profiles/r01/pmc_SQ_*_temporal.csv)"}
+        if n_gpus > 1:
+            out["phases"] = {"ring_ms": round(ph["ring_ms"], 4), "interior_ms": round(ph["interior_ms"], 4),
+                             "halo_ms": round(ph["halo_ms"], 4), "block_ms": round(ph["block_ms"], 4),
+                             "blocks": ph["blocks"], "exposed_ms": round(ph["block_ms"] - ph["interior_ms"], 4),
+                             "max_over_ranks": {"exposed_ms": round(exposed[0], 4), "block_ms": round(exposed[1], 4),
+                                                "halo_ms": round(exposed[2], 4)},
+                             "note": "per overlapped block (one halo exchange): rank 0's shards; exposed = block - "
+                                     "interior, the time the ring + halo add to the critical path"}
+        if parity is not None:
+            out["parity_vs_1gpu"] = parity
         if n_gpus == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
         print(json.dumps(out), flush=True)

@@ -241,6 +241,17 @@ int life_dev_kernel_stats(life_dev *d, double *avg_ms, int64_t *launches, double
  * of every updated cell's encoding per launch, so a temporally blocked launch
  * advancing K generations books its cells once, not K times. */
 int life_dev_kernel_work(life_dev *d, double *cell_updates_per_launch, double *valu_ops_per_launch);
+/* Partitioned shards, timing on: mean device time per overlapped block
+ * (one exchange period: 1 generation, or up to K with temporal layouts) of
+ * its phases, each shard's blocks averaged -- the boundary-ring kernels
+ * (compute stream), the interior kernel (second compute stream, concurrent),
+ * the halo exchange of the ring's new state (comm stream: pack, ncclSend /
+ * ncclRecv or local copies, unpack; from the moment the ring is done), and
+ * the whole block from the ring's start to the join of the three streams.
+ * block - interior is what the halo and ring add to the critical path (0 when
+ * fully hidden).  Zeros when no block was timed (unpartitioned grids). */
+int life_dev_phase_stats(life_dev *d, double *ring_ms, double *interior_ms, double *halo_ms, double *block_ms,
+                         int64_t *blocks);
 
 /* Stencil tuning for the whole process, per kernel family (-1: both): rows
  * each lane walks (16/32/64) and rows of loads kept in flight (2/4/8); 0

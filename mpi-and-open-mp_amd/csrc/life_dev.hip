@@ -67,6 +67,13 @@ struct TimedLaunch {
     int launches = 1;  // kernel launches between a and b (back-to-back on one stream)
 };
 
+// Event set of one overlapped block (timing on): ring kernels, interior
+// kernel, halo exchange, and the whole block on the compute stream.
+struct PhaseEvents {
+    hipEvent_t ring0 = nullptr, ring1 = nullptr, int0 = nullptr, int1 = nullptr, halo0 = nullptr,
+               halo1 = nullptr, end = nullptr;
+};
+
 struct Shard {
     int rank = 0;    // global shard rank (Cartesian rank, row-major coords)
     int device = 0;
@@ -88,6 +95,8 @@ struct Shard {
     std::vector<life_halo_op> plan;
     std::vector<TimedLaunch> timers;
     size_t timers_used = 0;
+    std::vector<PhaseEvents> phases;
+    size_t phases_used = 0;
 };
 
 }  // namespace
@@ -112,6 +121,9 @@ struct life_dev {
     double acc_bytes = 0.0;    // algorithmic HBM bytes of the timed launches
     double acc_updates = 0.0;  // cell-updates they performed
     double acc_valu = 0.0;     // VALU lane-ops they issue (model; 0 where not modelled)
+    // overlapped blocks of partitioned shards: summed ms per phase (timing on)
+    double ph_ring = 0.0, ph_int = 0.0, ph_halo = 0.0, ph_block = 0.0;
+    int64_t ph_blocks = 0;
 };
 
 namespace {
@@ -160,6 +172,9 @@ void shard_free(Shard &s) {
         if (t.a) (void)hipEventDestroy(t.a);
         if (t.b) (void)hipEventDestroy(t.b);
     }
+    for (auto &p : s.phases)
+        for (hipEvent_t e : {p.ring0, p.ring1, p.int0, p.int1, p.halo0, p.halo1, p.end})
+            if (e) (void)hipEventDestroy(e);
     for (uint8_t *p : {s.buf[0], s.buf[1], s.col_send, s.col_recv, s.sink, s.stage})
         if (p) (void)hipFree(p);
     if (s.d_count) (void)hipFree(s.d_count);
@@ -366,6 +381,43 @@ int harvest_timers(life_dev *d) {
     return LIFE_OK;
 }
 
+PhaseEvents *phase_slot(Shard &s, int *rc) {
+    *rc = LIFE_OK;
+    if (s.phases_used == s.phases.size()) {
+        PhaseEvents p;
+        for (hipEvent_t *e : {&p.ring0, &p.ring1, &p.int0, &p.int1, &p.halo0, &p.halo1, &p.end})
+            if (hipEventCreate(e) != hipSuccess) {
+                set_err("hipEventCreate failed");
+                *rc = LIFE_EHIP;
+                return nullptr;
+            }
+        s.phases.push_back(p);
+    }
+    return &s.phases[s.phases_used++];
+}
+
+int harvest_phases(life_dev *d) {
+    for (Shard &s : d->shards) {
+        HIPCHK(hipSetDevice(s.device));
+        for (size_t i = 0; i < s.phases_used; i++) {
+            const PhaseEvents &p = s.phases[i];
+            HIPCHK(hipEventSynchronize(p.end));
+            float r = 0.f, n = 0.f, h = 0.f, b = 0.f;
+            HIPCHK(hipEventElapsedTime(&r, p.ring0, p.ring1));
+            HIPCHK(hipEventElapsedTime(&n, p.int0, p.int1));
+            HIPCHK(hipEventElapsedTime(&h, p.halo0, p.halo1));
+            HIPCHK(hipEventElapsedTime(&b, p.ring0, p.end));
+            d->ph_ring += r;
+            d->ph_int += n;
+            d->ph_halo += h;
+            d->ph_block += b;
+            d->ph_blocks++;
+        }
+        s.phases_used = 0;
+    }
+    return LIFE_OK;
+}
+
 bool temporal(const life_dev *d) { return d->shards[0].lay.generations_per_exchange > 1; }
 
 // Launches up to 4 tile regions of the temporal stencil as ONE kernel on
@@ -410,6 +462,39 @@ int join_streams(Shard &s) {
     HIPCHK(hipStreamWaitEvent(s.stream, s.ev_halo, 0));
     HIPCHK(hipEventRecord(s.ev_join, s.stream));
     HIPCHK(hipStreamWaitEvent(s.stream2, s.ev_join, 0));
+    return LIFE_OK;
+}
+
+// Phase timing of one overlapped block (timing on): ring0 before the ring
+// kernels on the compute stream, ring1 after them; the comm stream waits for
+// the ring (ev_ring) and records halo0, then the exchange, halo1; the
+// interior kernel is bracketed on the second compute stream; `end` after the
+// join on the compute stream.  Without timing: just the ring -> comm order.
+int phase_begin(life_dev *d, Shard &s, PhaseEvents **pe) {
+    *pe = nullptr;
+    if (!d->timing) return LIFE_OK;
+    int rc;
+    *pe = phase_slot(s, &rc);
+    if (!*pe) return rc;
+    HIPCHK(hipEventRecord((*pe)->ring0, s.stream));
+    return LIFE_OK;
+}
+int phase_ring(Shard &s, PhaseEvents *pe) {
+    if (pe) HIPCHK(hipEventRecord(pe->ring1, s.stream));
+    HIPCHK(hipEventRecord(s.ev_ring, s.stream));
+    HIPCHK(hipStreamWaitEvent(s.comm_stream, s.ev_ring, 0));
+    if (pe) HIPCHK(hipEventRecord(pe->halo0, s.comm_stream));
+    return LIFE_OK;
+}
+int phase_end(life_dev *d, const std::vector<PhaseEvents *> &pe) {
+    for (size_t si = 0; si < d->shards.size(); ++si) {
+        Shard &s = d->shards[si];
+        HIPCHK(hipSetDevice(s.device));
+        HIPCHK(hipEventRecord(s.ev_halo, s.comm_stream));
+        if (pe[si]) HIPCHK(hipEventRecord(pe[si]->halo1, s.comm_stream));
+        CHK(join_streams(s));
+        if (pe[si]) HIPCHK(hipEventRecord(pe[si]->end, s.stream));
+    }
     return LIFE_OK;
 }
 
@@ -475,7 +560,9 @@ int next_block(const life_dev *d, int64_t remaining) {
 // partitioned: its "exchange" is the column copy.
 int generation_block(life_dev *d, int m) {
     const bool rx = d->dims[0] > 1 || self_wrap_x(d), ry = d->dims[1] > 1;
-    for (Shard &s : d->shards) {
+    std::vector<PhaseEvents *> pe(d->shards.size(), nullptr);
+    for (size_t si = 0; si < d->shards.size(); ++si) {
+        Shard &s = d->shards[si];
         HIPCHK(hipSetDevice(s.device));
         const int64_t K = s.lay.generations_per_exchange;
         // grid of units (tiles or strips x segments): NX x NY, unit height uh;
@@ -527,22 +614,20 @@ int generation_block(life_dev *d, int m) {
             if (ca > 0) ring[n++] = life::TileRegion{0, ca, ra, rb};
             if (cb < NX) ring[n++] = life::TileRegion{cb, NX, ra, rb};
         }
+        CHK(phase_begin(d, s, &pe[si]));
         CHK(launch(ring, n, false, s.stream));
-        HIPCHK(hipEventRecord(s.ev_ring, s.stream));
-        HIPCHK(hipStreamWaitEvent(s.comm_stream, s.ev_ring, 0));
+        CHK(phase_ring(s, pe[si]));
         const life::TileRegion inner{ca, cb, ra, rb};
+        if (pe[si]) HIPCHK(hipEventRecord(pe[si]->int0, s.stream2));
         if (rb > ra && cb > ca) CHK(launch(&inner, 1, true, s.stream2));
+        if (pe[si]) HIPCHK(hipEventRecord(pe[si]->int1, s.stream2));
     }
     if (!(rx || ry)) {
         for (Shard &s : d->shards) s.cur ^= 1;
         return LIFE_OK;
     }
     CHK(exchange(d, 1, true));
-    for (Shard &s : d->shards) {
-        HIPCHK(hipSetDevice(s.device));
-        HIPCHK(hipEventRecord(s.ev_halo, s.comm_stream));
-        CHK(join_streams(s));
-    }
+    CHK(phase_end(d, pe));
     for (Shard &s : d->shards) s.cur ^= 1;
     return LIFE_OK;
 }
@@ -561,8 +646,11 @@ int generation(life_dev *d) {
     // Ring first (cells whose 3x3 neighbourhood reaches a partitioned axis'
     // apron) on the compute stream, then the halo of the new state on the
     // comm stream; the interior runs concurrently on the second compute stream.
-    for (Shard &s : d->shards) {
+    std::vector<PhaseEvents *> pe(d->shards.size(), nullptr);
+    for (size_t si = 0; si < d->shards.size(); ++si) {
+        Shard &s = d->shards[si];
         HIPCHK(hipSetDevice(s.device));
+        CHK(phase_begin(d, s, &pe[si]));
         const int64_t U = s.lay.units, H = s.lay.h;
         const int64_t ra = ry ? 1 : 0, rb = ry ? H - 1 : H;  // interior rows
         if (ry) {
@@ -573,17 +661,14 @@ int generation(life_dev *d) {
             CHK(launch_region(d, s, life::Region{0, 1, ra, rb}, false, s.stream));
             if (U > 1) CHK(launch_region(d, s, life::Region{U - 1, U, ra, rb}, false, s.stream));
         }
-        HIPCHK(hipEventRecord(s.ev_ring, s.stream));
-        HIPCHK(hipStreamWaitEvent(s.comm_stream, s.ev_ring, 0));
+        CHK(phase_ring(s, pe[si]));
         const int64_t ua = rx ? 1 : 0, ub = rx ? U - 1 : U;
+        if (pe[si]) HIPCHK(hipEventRecord(pe[si]->int0, s.stream2));
         if (rb > ra && ub > ua) CHK(launch_region(d, s, life::Region{ua, ub, ra, rb}, true, s.stream2));
+        if (pe[si]) HIPCHK(hipEventRecord(pe[si]->int1, s.stream2));
     }
     CHK(exchange(d, 1, true));  // halo of nxt on the comm streams
-    for (Shard &s : d->shards) {
-        HIPCHK(hipSetDevice(s.device));
-        HIPCHK(hipEventRecord(s.ev_halo, s.comm_stream));
-        CHK(join_streams(s));
-    }
+    CHK(phase_end(d, pe));
     for (Shard &s : d->shards) s.cur ^= 1;
     return LIFE_OK;
 }
@@ -1042,12 +1127,28 @@ int life_dev_configure(life_dev *d, int option, int value) {
 int life_dev_set_timing(life_dev *d, int on) {
     if (!d) return LIFE_EINVAL;
     CHK(harvest_timers(d));
+    CHK(harvest_phases(d));
+    d->ph_ring = d->ph_int = d->ph_halo = d->ph_block = 0.0;
+    d->ph_blocks = 0;
     d->timing = on != 0;
     d->acc_ms = 0.0;
     d->acc_launches = 0;
     d->acc_bytes = 0.0;
     d->acc_updates = 0.0;
     d->acc_valu = 0.0;
+    return LIFE_OK;
+}
+
+int life_dev_phase_stats(life_dev *d, double *ring_ms, double *interior_ms, double *halo_ms, double *block_ms,
+                         int64_t *blocks) {
+    if (!d) return LIFE_EINVAL;
+    CHK(harvest_phases(d));
+    const double n = d->ph_blocks ? (double)d->ph_blocks : 1.0;
+    if (ring_ms) *ring_ms = d->ph_ring / n;
+    if (interior_ms) *interior_ms = d->ph_int / n;
+    if (halo_ms) *halo_ms = d->ph_halo / n;
+    if (block_ms) *block_ms = d->ph_block / n;
+    if (blocks) *blocks = d->ph_blocks;
     return LIFE_OK;
 }
 

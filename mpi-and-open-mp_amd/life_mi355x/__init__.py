@@ -52,7 +52,7 @@ ABI_SYMBOLS = (
     "life_dev_step", "life_dev_gather", "life_dev_live_count", "life_dev_sync",
     "life_dev_layout", "life_dev_world", "life_dev_set_timing", "life_dev_kernel_stats",
     "life_tune", "life_tune_temporal", "life_dev_configure", "life_dev_kernel_work", "life_dev_checksum",
-    "life_dev_gather_vtk", "life_dev_destroy", "life_measure_copy",
+    "life_dev_gather_vtk", "life_dev_destroy", "life_measure_copy", "life_dev_phase_stats",
 )
 
 
@@ -122,6 +122,7 @@ def _lib():
         L.life_dev_configure.argtypes = [vp, i32, i32]
         L.life_dev_kernel_stats.argtypes = [vp, P(ctypes.c_double), P(i64), P(ctypes.c_double)]
         L.life_dev_kernel_work.argtypes = [vp, P(ctypes.c_double), P(ctypes.c_double)]
+        L.life_dev_phase_stats.argtypes = [vp] + [P(ctypes.c_double)] * 4 + [P(i64)]
         L.life_tune.argtypes = [i32, i32, i32]
         L.life_tune_temporal.argtypes = [i32, i32]
         L.life_measure_copy.argtypes = [i32, i64, i32, P(ctypes.c_double)]
@@ -324,6 +325,14 @@ class Life:
         u, v = ctypes.c_double(), ctypes.c_double()
         _check(_lib().life_dev_kernel_work(self._h, ctypes.byref(u), ctypes.byref(v)), "kernel_work")
         return u.value, v.value
+
+    def phase_stats(self):
+        """Mean ms per overlapped block of the ring, interior, halo exchange
+        and whole block, and the number of blocks (life_dev_phase_stats)."""
+        v = [ctypes.c_double() for _ in range(4)]
+        n = ctypes.c_int64()
+        _check(_lib().life_dev_phase_stats(self._h, *[ctypes.byref(x) for x in v], ctypes.byref(n)), "phase_stats")
+        return dict(zip(("ring_ms", "interior_ms", "halo_ms", "block_ms"), (x.value for x in v)), blocks=n.value)
 
     def close(self) -> None:
         if self._h:
