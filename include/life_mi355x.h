@@ -111,7 +111,7 @@ int life_halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int k
  * (32-cell x-apron, K-row y-apron) K = LIFE_TEMPORAL_DEPTH (bit) or
  * LIFE_TEMPORAL_DEPTH_BYTE (byte), or 8/12/16/24/32 from the environment
  * variables of the same names. */
-#define LIFE_TEMPORAL_DEPTH 16
+#define LIFE_TEMPORAL_DEPTH 32
 #define LIFE_TEMPORAL_DEPTH_BYTE 32
 typedef struct {
     int64_t w, h;      /* owned block */
@@ -221,6 +221,13 @@ int life_dev_set_timing(life_dev *d, int on);
  * generations, life_kernels.hip tstep_kernel), measured faster.  Same
  * results either way. */
 #define LIFE_OPT_SWEEP 3
+/* LIFE_OPT_BLOCK_GENS: the tiled stencil's generations per launch at most
+ * (1..32, capped by generations_per_exchange; 0: the default, 20 for bits
+ * and 32 for bytes, or LIFE_BLOCK_GENS from the environment).  A step call of
+ * g generations runs ceil(g / max) launches of nearly equal size; a bit
+ * launch of m generations holds m ghost rows above and below each tile
+ * (tile height 8R - 2m), a byte launch K. */
+#define LIFE_OPT_BLOCK_GENS 5
 /* LIFE_OPT_SMALL_GRID value 3: the register-resident small-grid kernel
  * WINDOWED over several CUs whenever the shape allows
  * (life_kernels.hip rsmall_kernel<.., WIN>): ceil(h / own) workgroups, each

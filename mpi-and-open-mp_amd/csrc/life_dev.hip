@@ -15,6 +15,7 @@
 #include <rccl/rccl.h>
 #include <algorithm>
 #include <stdarg.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -101,6 +102,22 @@ struct Shard {
 
 }  // namespace
 
+// Tiles: generations per launch at most (the apron depth K allows up to K).
+// Bit tiles hold m ghost rows per window end, so longer launches mean more
+// ghost rows (2m of 8R) but fewer window loads / stores: 20 measured best at
+// 65536^2 (16 equal, 12 / 24 / 32 1-3 % slower; profiles/r02/block_gens.txt),
+// and a 20-generation call then runs as ONE launch.  Byte tiles are
+// HBM-bound below ~32 generations per pass: 32.  LIFE_BLOCK_GENS overrides
+// both at load time; 0 = per encoding.
+static const int kEnvBlockGens = [] {
+    const char *e = getenv("LIFE_BLOCK_GENS");
+    const int v = e ? atoi(e) : 0;
+    return v >= 1 && v <= 32 ? v : 0;
+}();
+static int default_block_gens(int kernel) {
+    return kEnvBlockGens ? kEnvBlockGens : (kernel == LIFE_KERNEL_BIT ? 20 : 32);
+}
+
 struct life_dev {
     int64_t nx = 0, ny = 0;
     int dims[2] = {1, 1};
@@ -110,6 +127,7 @@ struct life_dev {
     bool rank_mode = false;
     bool timing = false;
     bool overlap = true;
+    int block_gens = 0;  // tiles: generations per launch at most (LIFE_OPT_BLOCK_GENS; default_block_gens)
     bool sweep = false;  // temporal layouts: sweep_kernel (LIFE_OPT_SWEEP 1) or tstep_kernel tiles (0, default:
                          // faster by measurement, profiles/r02/sweep_ab.txt)
     int small_mode = 1;  // grids that fit one CU: 0 off, 1 VGPR kernel else LDS kernel, 2 LDS kernel,
@@ -435,7 +453,7 @@ int launch_tiles(life_dev *d, Shard &s, const life::TileRegion *r, int nreg, int
     HIPCHK(life::launch_tstep(s.lay, in, out, r, nreg, m, wrap_of(d), st));
     if (t) {
         HIPCHK(hipEventRecord(t->b, st));
-        const life::TileGeom g = life::tile_geom(s.lay);
+        const life::TileGeom g = life::tile_geom(s.lay, m);
         for (int k = 0; k < nreg; k++) {
             const int64_t xa = r[k].tx0 * g.words * 32, xb = std::min(r[k].tx1 * g.words * 32, s.lay.w);
             const int64_t ya = r[k].ty0 * g.rows, yb = std::min(r[k].ty1 * g.rows, s.lay.h);
@@ -539,7 +557,14 @@ int launch_sweeps(life_dev *d, Shard &s, const life::SweepGeom &g, const life::T
 int next_block(const life_dev *d, int64_t remaining) {
     const life_layout &L = d->shards[0].lay;
     const int K = L.generations_per_exchange;
-    if (!d->sweep) return (int)std::min<int64_t>(remaining, K);
+    if (!d->sweep) {
+        // tiles: ceil(remaining / bmax) launches of nearly equal size (a
+        // 20-generation call runs 10 + 10, not 16 + 4)
+        int bmax = std::min(K, 32);
+        if (d->block_gens > 0) bmax = std::min(bmax, d->block_gens);
+        const int64_t n = (remaining + bmax - 1) / bmax;
+        return (int)((remaining + n - 1) / n);
+    }
     const int kmax = life::sweep_max_stages(L);
     const int64_t n = (remaining + kmax - 1) / kmax;
     const int target = (int)((remaining + n - 1) / n);
@@ -582,7 +607,7 @@ int generation_block(life_dev *d, int m) {
                 cb = std::max(cb, ca);
             }
         } else {
-            const life::TileGeom g = life::tile_geom(s.lay);
+            const life::TileGeom g = life::tile_geom(s.lay, m);
             NX = g.ntx;
             NY = g.nty;
             uh = g.rows;
@@ -721,6 +746,7 @@ int life_dev_create_ex(int64_t nx, int64_t ny, int nshards, int dims0, int dims1
     d->dims[1] = dims[1];
     d->world = nshards;
     d->kernel = kernel;
+    d->block_gens = default_block_gens(kernel);
     std::vector<int> ranks, devices;
     for (int i = 0; i < nshards; i++) {
         ranks.push_back(i);
@@ -788,6 +814,7 @@ int life_dev_create_rank(int64_t nx, int64_t ny, int kernel, int rank, int world
     d->dims[1] = dims[1];
     d->world = world;
     d->kernel = kernel;
+    d->block_gens = default_block_gens(kernel);
     d->rank_mode = true;
     d->transport = LIFE_XPORT_RCCL;
     int rc = create_common(d, {rank}, {device});
@@ -1116,6 +1143,10 @@ int life_dev_configure(life_dev *d, int option, int value) {
         return LIFE_OK;
     }
     case LIFE_OPT_OVERLAP: d->overlap = value != 0; return LIFE_OK;
+    case LIFE_OPT_BLOCK_GENS:
+        if (value < 0 || value > 32) return LIFE_EINVAL;
+        d->block_gens = value > 0 ? value : default_block_gens(d->kernel);
+        return LIFE_OK;
     case LIFE_OPT_SWEEP:
         if (value < 0 || value > 1) return LIFE_EINVAL;
         d->sweep = value != 0;

@@ -46,9 +46,11 @@ struct StepTuning {
 StepTuning step_tuning(bool bit);
 void set_step_tuning(int kernel, int rows, int depth);  // kernel -1: both
 
-// Temporally blocked stencil (layouts with generations_per_exchange = K in
-// {8, 16}, either encoding): tiles of 62 32-cell word columns x `rows` rows
-// (one workgroup each), m <= K generations per launch from `in` to `out`.
+// Temporally blocked stencil (layouts with generations_per_exchange = K > 1,
+// either encoding): tiles of 62 32-cell word columns x `rows` rows (one
+// workgroup each), m <= min(K, 32) generations per launch from `in` to `out`;
+// a tile's window holds m ghost rows above and below, so the tile height
+// depends on m: tile_geom(L, m).
 constexpr int kMaxRegions = 4;  // regions one temporal launch may hold
 struct TileRegion {
     int64_t tx0, tx1, ty0, ty1;
@@ -56,7 +58,8 @@ struct TileRegion {
 struct TileGeom {
     int64_t words, rows, ntx, nty;
 };
-TileGeom tile_geom(const life_layout &L);
+TileGeom tile_geom(const life_layout &L, int m);
+int tile_ghost(const life_layout &L, int m);  // ghost rows per window end: m (bit) or K (byte)
 // Rows a temporally blocked buffer is allocated beyond its layout's `rows`:
 // the last tile's window (<= 8 waves x 96 rows) may read past the bottom
 // apron without clamping.

@@ -247,7 +247,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs a) {
 //
 //  * sweep_kernel (default): one WAVE per column strip x row segment, the
 //    m generations pipelined down the segment (see below);
-//  * tstep_kernel: one 8-wave workgroup per 62-word x (8R - 2K)-row tile,
+//  * tstep_kernel: one 8-wave workgroup per 62-word x (8R - 2m)-row tile,
 //    all m generations of the tile in registers with one barrier per
 //    generation (LIFE_OPT_SWEEP 0).
 
@@ -259,7 +259,7 @@ struct TArgs {
     // up to kMaxRegions tile regions in one launch (the boundary ring of a
     // partitioned shard); workgroup b belongs to the region with first[k] <= b
     int64_t tx0[kMaxRegions], tx1[kMaxRegions], ty0[kMaxRegions], ty1[kMaxRegions], first[kMaxRegions + 1];
-    int32_t nreg, m;
+    int32_t nreg, m;  // generations of the launch = ghost rows at each end of a window
 };
 
 // Neighbour word from the left lane (DPP wave_shr:1, bound_ctrl: lane 0 reads
@@ -283,7 +283,8 @@ __device__ __forceinline__ void bit_hsum(uint32_t v, uint32_t &s0, uint32_t &s1)
 // tstep_kernel: one workgroup owns a tile of 62 word columns x T owned rows.
 // Its kStackWaves waves are stacked vertically: wave i holds window rows
 // [i*R, (i+1)*R) of a (kStackWaves*R)-row window that starts K rows above the
-// tile (T = kStackWaves*R - 2K), one 32-cell word per lane and register row
+// tile (T = kStackWaves*R - 2m for a launch of m generations), one 32-cell
+// word per lane and register row
 // (lane l holds word column 62*tx + l - 1; lanes 0 and 63 are the one-word
 // x-apron of the tile).  Each generation a wave publishes the horizontal sums
 // of its first and last row in LDS, one barrier, and takes its neighbours'
@@ -292,11 +293,17 @@ __device__ __forceinline__ void bit_hsum(uint32_t v, uint32_t &s0, uint32_t &s1)
 // <= 32 bits after K generations), so rows [K, K+T) of lanes 1..62 are exact.
 // Bit: centred frame (bit_hsum); byte: drifting frame (bit_hsum_drift; +2 %
 // there, -1 % for bit: profiles/r01/drift_ab.jsonl).
-template <bool BYTE, int R, int K, bool WRAPX, bool WRAPY>
+template <bool BYTE, int R, int GK, bool WRAPX, bool WRAPY>
 __global__ __launch_bounds__(64 * kStackWaves, 4) void tstep_kernel(TArgs a) {  // 4 waves/SIMD: 2 tiles per CU
-    static_assert(R >= 3 && K >= 1 && K <= 32, "window");
+    static_assert(R >= 3 && GK >= 0 && GK <= 32, "window");
     constexpr int NW = kStackWaves;
-    constexpr int T = NW * R - 2 * K;
+    // the window's ghost rows at each end: GK, or (GK = 0) the launch's
+    // generations m <= 32 (checked on the host); after m generations rows
+    // [ghost, NW*R - ghost) are exact.  The byte tiles keep a compile-time
+    // ghost depth: with a runtime one they ran 29 % slower (profiles/r02/
+    // ghost_ab.txt); the bit tiles run the same either way.
+    const int K = GK > 0 ? GK : a.m;
+    const int T = NW * R - 2 * K;
     __shared__ uint32_t xch[2][NW][4][64];  // [parity][wave][top s0/s1, bottom s0/s1][lane]
     constexpr bool DRIFT = BYTE;
     const int lane = threadIdx.x & 63;
@@ -965,9 +972,10 @@ namespace {
 struct Tunings {
     StepTuning t[2];  // [0] byte, [1] bit
     // temporal stencil: register rows per wave (window = kStackWaves * rows,
-    // tile = window - 2K), per encoding [byte, bit]; fastest measured at
-    // 65536^2 with K = 32 and hsum mode 2 (profiles/r01/tune_stacked_*_k32_hsum2.jsonl)
-    int nr[2] = {32, 48};
+    // tile = window - 2 ghost), per encoding [byte, bit]; fastest measured at
+    // 32768^2 and 65536^2 with 20 (bit) / 32 (byte) generations per launch
+    // (profiles/r02/tile_rows.txt)
+    int nr[2] = {48, 48};
     Tunings() : t{{64, 2}, {16, 8}} {
         for (StepTuning &v : t) {
             if (const char *e = getenv("LIFE_STEP_ROWS")) v.rows = atoi(e);
@@ -1069,37 +1077,39 @@ hipError_t launch_step(const life_layout &L, const uint8_t *in, uint8_t *out, ui
 }
 
 namespace {
-template <bool BYTE, int R, int K>
+template <bool BYTE, int R, int GK>
 hipError_t launch_t(const TArgs &a, Wrap wrap, unsigned grid, hipStream_t s) {
     constexpr unsigned kThreads = 64 * kStackWaves;
     if (wrap.x && wrap.y)
-        tstep_kernel<BYTE, R, K, true, true><<<grid, kThreads, 0, s>>>(a);
+        tstep_kernel<BYTE, R, GK, true, true><<<grid, kThreads, 0, s>>>(a);
     else if (wrap.x)
-        tstep_kernel<BYTE, R, K, true, false><<<grid, kThreads, 0, s>>>(a);
+        tstep_kernel<BYTE, R, GK, true, false><<<grid, kThreads, 0, s>>>(a);
     else if (wrap.y)
-        tstep_kernel<BYTE, R, K, false, true><<<grid, kThreads, 0, s>>>(a);
+        tstep_kernel<BYTE, R, GK, false, true><<<grid, kThreads, 0, s>>>(a);
     else
-        tstep_kernel<BYTE, R, K, false, false><<<grid, kThreads, 0, s>>>(a);
+        tstep_kernel<BYTE, R, GK, false, false><<<grid, kThreads, 0, s>>>(a);
     return hipGetLastError();
 }
 
-template <bool BYTE, int K>
+template <bool BYTE, int GK>
 hipError_t launch_k(const TArgs &a, Wrap wrap, unsigned grid, hipStream_t s) {
     switch (temporal_rows(!BYTE)) {
-    case 32: return launch_t<BYTE, 32, K>(a, wrap, grid, s);
-    case 40: return launch_t<BYTE, 40, K>(a, wrap, grid, s);
-    case 56: return launch_t<BYTE, 56, K>(a, wrap, grid, s);
-    case 64: return launch_t<BYTE, 64, K>(a, wrap, grid, s);
-    case 96: return launch_t<BYTE, 96, K>(a, wrap, grid, s);
-    default: return launch_t<BYTE, 48, K>(a, wrap, grid, s);
+    case 32: return launch_t<BYTE, 32, GK>(a, wrap, grid, s);
+    case 40: return launch_t<BYTE, 40, GK>(a, wrap, grid, s);
+    case 56: return launch_t<BYTE, 56, GK>(a, wrap, grid, s);
+    case 64: return launch_t<BYTE, 64, GK>(a, wrap, grid, s);
+    case 96: return launch_t<BYTE, 96, GK>(a, wrap, grid, s);
+    default: return launch_t<BYTE, 48, GK>(a, wrap, grid, s);
     }
 }
 }  // namespace
 
-TileGeom tile_geom(const life_layout &L) {
+int tile_ghost(const life_layout &L, int m) { return is_bit(L) ? m : L.generations_per_exchange; }
+
+TileGeom tile_geom(const life_layout &L, int m) {
     TileGeom g;
     g.words = 62;
-    g.rows = (int64_t)kStackWaves * temporal_rows(is_bit(L)) - 2 * (int64_t)L.generations_per_exchange;
+    g.rows = (int64_t)kStackWaves * temporal_rows(is_bit(L)) - 2 * (int64_t)tile_ghost(L, m);
     g.ntx = ((L.w + 31) / 32 + g.words - 1) / g.words;
     g.nty = (L.h + g.rows - 1) / g.rows;
     return g;
@@ -1108,7 +1118,11 @@ TileGeom tile_geom(const life_layout &L) {
 hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, const TileRegion *r, int nreg,
                         int m, Wrap wrap, hipStream_t s) {
     const int K = L.generations_per_exchange;
-    if (nreg < 0 || nreg > kMaxRegions || m > K || (K != 16 && K != 24 && K != 32) || L.yapron != K)
+    // m <= 32: the tile's edge lanes absorb at most 32 wrong bits; m <= the
+    // apron depth a partitioned axis provides
+    if (nreg < 0 || nreg > kMaxRegions || m > K || m > 32 || K < 2 || L.yapron != K ||
+        kStackWaves * temporal_rows(is_bit(L)) - 2 * tile_ghost(L, m) < 1 ||
+        (!is_bit(L) && K != 16 && K != 32))
         return hipErrorInvalidValue;
     TArgs a;
     a.in = in;
@@ -1132,11 +1146,8 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
     }
     if (a.nreg == 0 || m <= 0) return hipSuccess;
     const unsigned grid = (unsigned)a.first[a.nreg];  // one workgroup per tile
-    if (is_bit(L))
-        return K == 16 ? launch_k<false, 16>(a, wrap, grid, s)
-                       : K == 24 ? launch_k<false, 24>(a, wrap, grid, s) : launch_k<false, 32>(a, wrap, grid, s);
-    return K == 16 ? launch_k<true, 16>(a, wrap, grid, s)
-                   : K == 24 ? launch_k<true, 24>(a, wrap, grid, s) : launch_k<true, 32>(a, wrap, grid, s);
+    if (is_bit(L)) return launch_k<false, 0>(a, wrap, grid, s);
+    return K == 16 ? launch_k<true, 16>(a, wrap, grid, s) : launch_k<true, 32>(a, wrap, grid, s);
 }
 
 int reg_small_rows(const life_layout &L) {

@@ -69,7 +69,10 @@ static int env_depth(const char *name, int dflt) {
 }
 static int temporal_depth(int kernel) {
     static const int kbit = env_depth("LIFE_TEMPORAL_DEPTH", LIFE_TEMPORAL_DEPTH);
-    static const int kbyte = env_depth("LIFE_TEMPORAL_DEPTH_BYTE", LIFE_TEMPORAL_DEPTH_BYTE);
+    static const int kbyte = [] {  // the byte tiles are built for 16 or 32 ghost rows
+        const int v = env_depth("LIFE_TEMPORAL_DEPTH_BYTE", LIFE_TEMPORAL_DEPTH_BYTE);
+        return v == 1 || v == 16 ? v : 32;
+    }();
     return kernel == LIFE_KERNEL_BIT ? kbit : kbyte;
 }
 

@@ -86,10 +86,15 @@ def test_timing_stats(gpu, kernel, nx, gens, sweep):
     lane-ops are modelled for the temporal kernels only."""
     K = gpu.TEMPORAL_DEPTH[kernel]
     temporal = nx >= 32
-    # sweep launches: ceil(gens / kmax) nearly equal ones (kmax = K capped by
-    # the largest sweep instance, 16); tiles: K, K, ..., rest
-    kmax = min(K, 16) if sweep else K
-    launches = (-(-gens // kmax)) if temporal else gens
+    # ceil(gens / bmax) launches of nearly equal size; bmax: sweep = K capped
+    # by the largest sweep instance (16), tiles = K capped by BLOCK_GENS
+    bmax = min(K, 16) if sweep else min(K, 32, gpu.BLOCK_GENS[kernel])
+    sizes, left = [], gens
+    while temporal and left:
+        n = -(-left // bmax)
+        sizes.append(-(-left // n))
+        left -= sizes[-1]
+    launches = len(sizes) if temporal else gens
     with gpu.Life(nx, 4096, kernel=kernel, small_grid=False, sweep=sweep) as life:
         life.fill_random(1)
         life.set_timing(True)
@@ -100,13 +105,17 @@ def test_timing_stats(gpu, kernel, nx, gens, sweep):
         assert n * b == pytest.approx(nx * 4096 * launches * (0.25 if kernel == "bit" else 2.0))
         assert n * upd == pytest.approx(nx * 4096 * gens)
         assert (valu > 0) == temporal
-        if temporal and not sweep:  # 3 x ceil(4096 / (8 waves x R rows - 2K)) tiles of 62 words, 64 lanes;
+        if temporal and not sweep:  # 3 x ceil(4096 / (8 waves x R rows - 2m)) tiles of 62 words, 64 lanes;
             # byte: + pack/unpack (35 ops per register row per launch)
             R = gpu.TEMPORAL_ROWS[kernel]
-            tiles = 3 * -(-4096 // (8 * R - 2 * K))
-            # 13 VALU + 1 LDS per row; byte: drifting frame, 12 VALU + 1 LDS
-            per_row = (12 if kernel == "byte" else 13) * gens + (35 * launches if kernel == "byte" else 0)
-            assert n * valu == pytest.approx(tiles * 64 * 8 * R * per_row)
+            want = 0
+            for m in sizes:
+                ghost = m if kernel == "bit" else K  # byte tiles: compile-time ghost depth K
+                tiles = 3 * -(-4096 // (8 * R - 2 * ghost))
+                # 13 VALU + 1 LDS per row; byte: drifting frame, 12 VALU + 1 LDS
+                per_row = (12 if kernel == "byte" else 13) * m + (35 if kernel == "byte" else 0)
+                want += tiles * 64 * 8 * R * per_row
+            assert n * valu == pytest.approx(want)
         if temporal and sweep:
             # 12 VALU per 64-lane x 32-cell stage-step = 0.375 lane-ops per
             # cell-update, plus ghost work (x: 2 of 64 lanes + overhang; y:
