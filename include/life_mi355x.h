@@ -196,6 +196,12 @@ int64_t life_dev_live_count(life_dev *d);
 int life_dev_checksum(life_dev *d, uint64_t *sum);
 
 int life_dev_sync(life_dev *d);
+/* life_dev_sync, then (rank mode) an all-reduce every rank joins: the
+ * synchronisation the reference gets from its blocking MPI calls; the driver
+ * brackets its timer with it.  Blocking. */
+int life_dev_barrier(life_dev *d);
+/* Visible HIP devices (hipGetDeviceCount), or a negative LIFE_E* code. */
+int life_device_count(void);
 int life_dev_layout(life_dev *d, int local_shard, life_layout *out);
 int life_dev_world(life_dev *d, int *world, int *dims0, int *dims1, int *nlocal, int *transport);
 

@@ -970,6 +970,30 @@ int life_dev_step(life_dev *d, int64_t generations) {
     return LIFE_OK;
 }
 
+int life_device_count(void) {
+    int n = 0;
+    const hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        set_err("hipGetDeviceCount: %s", hipGetErrorString(e));
+        return LIFE_EHIP;
+    }
+    return n;
+}
+
+int life_dev_barrier(life_dev *d) {
+    if (!d) return LIFE_EINVAL;
+    CHK(life_dev_sync(d));
+    if (d->rank_mode)
+        for (Shard &s : d->shards)
+            if (s.comm) {
+                // an all-reduce every rank must join: no rank leaves before all arrived
+                HIPCHK(hipSetDevice(s.device));
+                NCCLCHK(ncclAllReduce(s.d_count, s.d_count, 1, ncclUint64, ncclSum, s.comm, s.stream));
+                HIPCHK(hipStreamSynchronize(s.stream));
+            }
+    return LIFE_OK;
+}
+
 int life_dev_sync(life_dev *d) {
     if (!d) return LIFE_EINVAL;
     for (Shard &s : d->shards) {
@@ -1045,23 +1069,42 @@ int gather_impl(life_dev *d, uint8_t *out, int bpc) {
         return LIFE_OK;
     }
     HIPCHK(hipStreamSynchronize(s.stream));
-    CHK(place(s.lay, stage));
     int64_t maxb = 0;
     for (int r = 0; r < d->world; r++) {
         life_layout L;
         CHK(life_layout_query(d->nx, d->ny, d->dims[0], d->dims[1], r, d->kernel, &L));
         if (L.w * L.h > maxb) maxb = L.w * L.h;
     }
-    // the root's own block is placed: its staging now receives the others'
-    CHK(stage_buffer(s, (size_t)(maxb * bpc), &stage));
-    for (int r = 0; r < d->world; r++) {
-        if (r == root) continue;
-        life_layout L;
-        CHK(life_layout_query(d->nx, d->ny, d->dims[0], d->dims[1], r, d->kernel, &L));
-        NCCLCHK(ncclRecv(stage, (size_t)(L.w * L.h * bpc), ncclUint8, r, s.comm, s.stream));
-        HIPCHK(hipStreamSynchronize(s.stream));
-        CHK(place(L, stage));
+    // The root's own block sits in the front of the staging buffer; two
+    // receive slots follow.  Block k+1 arrives over RCCL (non-blocking
+    // stream) while the host copies block k out of the other slot (a
+    // blocking copy into the caller's pageable memory), so the fan-in of
+    // world-1 blocks is not serialised behind the D2H copies.
+    const size_t slot = (size_t)(maxb * bpc);
+    {
+        // grow keeping the exported block: copy it to the host first
+        CHK(place(s.lay, stage));
+        CHK(stage_buffer(s, 2 * slot, &stage));
     }
+    std::vector<int> peers;
+    for (int r = 0; r < d->world; r++)
+        if (r != root) peers.push_back(r);
+    auto layout_of = [&](int r, life_layout *L) { return life_layout_query(d->nx, d->ny, d->dims[0], d->dims[1], r,
+                                                                           d->kernel, L); };
+    for (size_t k = 0; k < peers.size(); k++) {
+        life_layout L;
+        CHK(layout_of(peers[k], &L));
+        if (k == 0) NCCLCHK(ncclRecv(stage, (size_t)(L.w * L.h * bpc), ncclUint8, peers[0], s.comm, s.stream));
+        HIPCHK(hipStreamSynchronize(s.stream));  // block k is in slot k % 2
+        if (k + 1 < peers.size()) {
+            life_layout Ln;
+            CHK(layout_of(peers[k + 1], &Ln));
+            NCCLCHK(ncclRecv(stage + ((k + 1) % 2) * slot, (size_t)(Ln.w * Ln.h * bpc), ncclUint8, peers[k + 1],
+                             s.comm, s.stream));
+        }
+        CHK(place(L, stage + (k % 2) * slot));
+    }
+    HIPCHK(hipStreamSynchronize(s.stream));
     return LIFE_OK;
 }
 }  // namespace
@@ -1138,6 +1181,12 @@ int life_dev_configure(life_dev *d, int option, int value) {
     case LIFE_OPT_SMALL_WINDOW: {
         const int R = value >> 8, K = value & 255;  // R = 0 (value 0): automatic
         if (value != 0 && (K < 1 || R < 1 || R > 8 || R == 7)) return LIFE_EINVAL;
+        // a window the shard cannot hold (own = strips*R - 2K rows < 1, or
+        // >= h) would silently fall back to the unwindowed kernel: refuse it
+        if (value != 0 && life::reg_win_plan(d->shards[0].lay, R, K).blocks == 0) {
+            set_err("small-grid window R=%d K=%d does not fit this grid", R, K);
+            return LIFE_EINVAL;
+        }
         d->win_rows = R;
         d->win_halo = K;
         return LIFE_OK;

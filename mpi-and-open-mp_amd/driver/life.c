@@ -23,6 +23,14 @@
  *                     packed binary dump vtk/life_%06d.bits (checkpoint)
  *   --resume FILE     start from a .bits dump instead of the .cfg cells
  *   --live            print the live-cell count after the run to stderr
+ *   --rank-mode       one-process-per-GPU mode even without a launcher (world 1)
+ *
+ * Under a launcher -- `torchrun --nproc-per-node P`, `mpirun -np P`
+ * (MPICH: PMI_RANK/PMI_SIZE, Open MPI: OMPI_COMM_WORLD_*), as the reference
+ * is run (3-life/job_life.sh:8) -- every process drives the one Cartesian
+ * block of its rank on GPU LOCAL_RANK; the RCCL unique id goes from rank 0 to
+ * the others over TCP (bootstrap.c); rank P-1 (the root of life_collect,
+ * life_cart.c:283-286) writes the frames and prints the time.
  *
  * Frames: the VTK cell text is formatted on the device
  * (life_dev_gather_vtk) and written while the next generations run (the
@@ -45,6 +53,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include "bootstrap.h"
 #include "life_mi355x.h"
 
 static void die(const char *what, int rc) {
@@ -118,7 +127,9 @@ static void *parse_cells(void *arg) {
             jb->status = 2;
             return NULL;
         }
-        jb->grid[wrapi(j, jb->ny) * jb->nx + wrapi(i, jb->nx)] = 1; /* u0[ind(i, j)] = 1 */
+        /* u0[ind(i, j)] = 1; threads may store the same cell (duplicates,
+         * wrapped coordinates): relaxed atomic stores, no data race */
+        __atomic_store_n(&jb->grid[wrapi(j, jb->ny) * jb->nx + wrapi(i, jb->nx)], (uint8_t)1, __ATOMIC_RELAXED);
     }
     jb->status = 0;
     return NULL;
@@ -237,11 +248,11 @@ static int save_bits(const char *path, int64_t nx, int64_t ny, int64_t gen, cons
     return fclose(f) == 0 && ok ? LIFE_OK : LIFE_EIO;
 }
 
-static int load_bits(const char *path, int64_t *nx, int64_t *ny, uint8_t **grid) {
+static int load_bits(const char *path, int64_t *nx, int64_t *ny, int64_t *gen, uint8_t **grid) {
     FILE *f = fopen(path, "r");
     if (!f) return LIFE_EIO;
     long long v, a, b, g;
-    if (fscanf(f, "LIFEBITS %lld %lld %lld %lld", &v, &a, &b, &g) != 4 || v != 1 || a <= 0 || b <= 0 ||
+    if (fscanf(f, "LIFEBITS %lld %lld %lld %lld", &v, &a, &b, &g) != 4 || v != 1 || a <= 0 || b <= 0 || g < 0 ||
         fgetc(f) != '\n') {
         fclose(f);
         return LIFE_EIO;
@@ -262,13 +273,14 @@ static int load_bits(const char *path, int64_t *nx, int64_t *ny, uint8_t **grid)
     }
     *nx = a;
     *ny = b;
+    *gen = g;
     *grid = out;
     return LIFE_OK;
 }
 
 int main(int argc, char **argv) {
     const char *cfg_path = NULL, *resume = NULL;
-    int gpus = 1, kernel = LIFE_KERNEL_BIT, vtk = 1, live = 0, have_random = 0, bits = 0;
+    int gpus = 1, kernel = LIFE_KERNEL_BIT, vtk = 1, live = 0, have_random = 0, bits = 0, force_rank = 0;
     int partition = LIFE_PARTITION_CART;
     long long o_nx = -1, o_ny = -1, o_steps = -1, o_save = -1;
     unsigned long long seed = 0;
@@ -296,13 +308,21 @@ int main(int argc, char **argv) {
             have_random = 1;
             char *end;
             seed = strtoull(argv[++a], &end, 10);
-            if (*end == ',') density = atof(end + 1);
+            if (*end == ',') {
+                char *dend;
+                density = strtod(end + 1, &dend);
+                if (*dend || !(density >= 0.0 && density <= 1.0)) {
+                    fprintf(stderr, "life_mi355x: --random density must be in [0, 1]\n");
+                    return 1;
+                }
+            }
         } else if (!strcmp(s, "--no-vtk")) vtk = 0;
         else if (!strcmp(s, "--format") && more) {
             const char *fm = argv[++a];
             bits = !strcmp(fm, "bits") ? 1 : !strcmp(fm, "vtk") ? 0 : -1;
         } else if (!strcmp(s, "--resume") && more) resume = argv[++a];
         else if (!strcmp(s, "--live")) live = 1;
+        else if (!strcmp(s, "--rank-mode")) force_rank = 1;
         else if (s[0] != '-' && !cfg_path) cfg_path = s;
         else {
             cfg_path = NULL;
@@ -318,6 +338,21 @@ int main(int argc, char **argv) {
         fprintf(stderr, "life_mi355x: bad --kernel/--gpus/--format/--partition\n");
         return 1;
     }
+    /* one process per GPU under a launcher (life_cart.c:114-115 takes rank and
+     * size from MPI; here from the launcher's environment) */
+    int rank = 0, world = 1, local_rank = 0;
+    const int launched = life_launcher_ranks(&rank, &world, &local_rank);
+    if (launched < 0) {
+        fprintf(stderr, "life_mi355x: inconsistent launcher rank variables\n");
+        return 1;
+    }
+    const int rank_mode = launched == 1 || force_rank;
+    if (rank_mode && gpus != 1) {
+        fprintf(stderr, "life_mi355x: --gpus drives several GPUs from one process; under a launcher every "
+                        "rank drives its own GPU (drop --gpus)\n");
+        return 1;
+    }
+    const int root = world - 1; /* life_collect's root: cart rank (dims0-1, dims1-1) = size-1 */
 
     cfg_t c = {0, 1, 0, 0, NULL};
     if (cfg_path && load_cfg(cfg_path, &c, resume ? -1 : o_nx, resume ? -1 : o_ny) != LIFE_OK) {
@@ -325,7 +360,8 @@ int main(int argc, char **argv) {
         return 1;
     }
     uint8_t *resumed = NULL;
-    if (resume && load_bits(resume, &c.nx, &c.ny, &resumed) != LIFE_OK) {
+    int64_t gen0 = 0; /* generation the run starts from (a --resume dump's) */
+    if (resume && load_bits(resume, &c.nx, &c.ny, &gen0, &resumed) != LIFE_OK) {
         fprintf(stderr, "life_mi355x: cannot read dump '%s'\n", resume);
         return 1;
     }
@@ -341,16 +377,41 @@ int main(int argc, char **argv) {
 
     life_dev *d = NULL;
     int dims[2];
-    int rc = life_dims_choose(c.nx, c.ny, gpus, partition, dims);
-    if (rc == LIFE_OK) rc = life_dev_create_ex(c.nx, c.ny, gpus, dims[0], dims[1], kernel, LIFE_XPORT_AUTO, &d);
+    int rc = life_dims_choose(c.nx, c.ny, rank_mode ? world : gpus, partition, dims);
+    if (rc == LIFE_OK && rank_mode) {
+        uint8_t uid[LIFE_UID_BYTES];
+        memset(uid, 0, sizeof uid);
+        if (rank == 0 && (rc = life_get_unique_id(uid)) != LIFE_OK) die("unique id", rc);
+        if (life_bootstrap_id(rank, world, uid, 120.0) != 0) {
+            fprintf(stderr, "life_mi355x: rank %d/%d: RCCL id bootstrap over TCP failed\n", rank, world);
+            return 1;
+        }
+        const int ndev = life_device_count();
+        if (ndev <= 0) die("no HIP device", LIFE_EHIP);
+        /* RCCL prints its version banner to stdout when a communicator is
+         * made; stdout carries only the elapsed time (as the reference's,
+         * which run_life.sh appends to times.txt): send the banner to stderr */
+        fflush(stdout);
+        const int saved = dup(STDOUT_FILENO);
+        if (saved >= 0) dup2(STDERR_FILENO, STDOUT_FILENO);
+        rc = life_dev_create_rank(c.nx, c.ny, kernel, rank, world, dims[0], dims[1], uid, local_rank % ndev, &d);
+        fflush(stdout);
+        if (saved >= 0) {
+            dup2(saved, STDOUT_FILENO);
+            close(saved);
+        }
+    } else if (rc == LIFE_OK) {
+        rc = life_dev_create_ex(c.nx, c.ny, gpus, dims[0], dims[1], kernel, LIFE_XPORT_AUTO, &d);
+    }
     if (rc) die("create", rc);
+    const int writer = !rank_mode || rank == root; /* the process that writes frames and prints */
     uint8_t *grid = NULL; /* dense cells: bits frames */
     char *body = NULL;    /* VTK cell text */
-    if (vtk && bits) {
+    if (vtk && bits && writer) {
         grid = (uint8_t *)calloc((size_t)(c.nx * c.ny), 1);
         if (!grid) die("host grid", LIFE_ENOMEM);
     }
-    if (vtk && !bits) {
+    if (vtk && !bits && writer) {
         body = (char *)malloc((size_t)(2 * c.nx * c.ny));
         if (!body) die("host frame", LIFE_ENOMEM);
     }
@@ -367,12 +428,15 @@ int main(int argc, char **argv) {
     c.grid = NULL;
 
     /* life_cart.c:62-80: the timer starts after init and covers the frame
-     * collects + VTK writes and every generation. */
+     * collects + VTK writes and every generation.  Generations and frame
+     * numbers are absolute: a resumed run continues the dump's sequence and
+     * --steps counts from generation 0. */
+    if ((rc = life_dev_barrier(d))) die("barrier", rc);
     const double t0 = now_s();
     char path[64];
-    for (int64_t i = 0; i < c.steps;) {
+    for (int64_t i = gen0; i < c.steps;) {
         const int save = vtk && i % c.save_steps == 0;
-        if (save) { /* collect (blocking), then write it while the GPU steps on */
+        if (save) { /* collect (blocking, every rank), then write it while the GPU steps on */
             if ((rc = bits ? life_dev_gather(d, grid) : life_dev_gather_vtk(d, body))) die("gather", rc);
             snprintf(path, sizeof path, bits ? "vtk/life_%06lld.bits" : "vtk/life_%06lld.vtk", (long long)i);
         }
@@ -382,14 +446,18 @@ int main(int argc, char **argv) {
             if (to_save < n) n = to_save;
         }
         if ((rc = life_dev_step(d, n))) die("step", rc); /* asynchronous */
-        if (save && (rc = bits ? save_bits(path, c.nx, c.ny, i, grid) : save_vtk(path, c.nx, c.ny, body)))
+        if (save && writer && (rc = bits ? save_bits(path, c.nx, c.ny, i, grid) : save_vtk(path, c.nx, c.ny, body)))
             die(path, rc);
         i += n;
     }
     if ((rc = life_dev_sync(d))) die("sync", rc);
+    if ((rc = life_dev_barrier(d))) die("barrier", rc);
     const double t1 = now_s();
-    printf("%f\n", t1 - t0);
-    if (live) fprintf(stderr, "live %lld\n", (long long)life_dev_live_count(d));
+    if (writer) printf("%f\n", t1 - t0);
+    if (live) {
+        const int64_t n = life_dev_live_count(d); /* collective in rank mode */
+        if (writer) fprintf(stderr, "live %lld\n", (long long)n);
+    }
     life_dev_destroy(d);
     free(grid);
     free(body);

@@ -23,7 +23,9 @@ no HIP device is present.
 from __future__ import annotations
 
 import ctypes
+import importlib.abc
 import os
+import sys
 
 import numpy as np
 
@@ -54,6 +56,7 @@ ABI_SYMBOLS = (
     "life_dev_layout", "life_dev_world", "life_dev_set_timing", "life_dev_kernel_stats",
     "life_tune", "life_tune_temporal", "life_dev_configure", "life_dev_kernel_work", "life_dev_checksum",
     "life_dev_gather_vtk", "life_dev_destroy", "life_measure_copy", "life_dev_phase_stats",
+    "life_dev_barrier", "life_device_count",
 )
 
 
@@ -85,12 +88,31 @@ class Layout(ctypes.Structure):
 _LIB = None
 
 
+class _TorchAfterLibraryGuard(importlib.abc.MetaPathFinder):
+    """Refuses `import torch` once liblife_mi355x.so is loaded:
+    the library binds /opt/rocm's libamdhip64.so.7; torch links its bundled HIP
+    runtime by the unversioned name, so importing it afterwards maps a SECOND
+    runtime into the process and it dies with a double free at exit.  With
+    torch imported first, the library binds torch's runtime and all is well."""
+
+    MESSAGE = ("life_mi355x: liblife_mi355x.so is already loaded with /opt/rocm's HIP runtime; importing torch now "
+               "would map torch's bundled HIP runtime as a second copy (the process aborts with a double free at "
+               "exit).  Import torch before the first life_mi355x device call, or not at all.")
+
+    def find_spec(self, name, path, target=None):
+        if name == "torch" or name.startswith("torch."):
+            raise ImportError(self.MESSAGE)
+        return None
+
+
 def _lib():
     global _LIB
     if _LIB is None:
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} is not built: run `make -C mpi-and-open-mp_amd` "
                               "or __graft_entry__.build()")
+        if "torch" not in sys.modules and not any(isinstance(f, _TorchAfterLibraryGuard) for f in sys.meta_path):
+            sys.meta_path.insert(0, _TorchAfterLibraryGuard())
         L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
         i64, i32, vp = ctypes.c_int64, ctypes.c_int, ctypes.c_void_p
         P = ctypes.POINTER
@@ -116,6 +138,8 @@ def _lib():
         L.life_dev_live_count.argtypes = [vp]
         L.life_dev_live_count.restype = i64
         L.life_dev_sync.argtypes = [vp]
+        L.life_dev_barrier.argtypes = [vp]
+        L.life_device_count.argtypes = []
         L.life_dev_checksum.argtypes = [vp, P(ctypes.c_uint64)]
         L.life_dev_layout.argtypes = [vp, i32, P(Layout)]
         L.life_dev_world.argtypes = [vp] + [P(ctypes.c_int)] * 5
@@ -301,6 +325,10 @@ class Life:
 
     def sync(self) -> None:
         _check(_lib().life_dev_sync(self._h), "sync")
+
+    def barrier(self) -> None:
+        """life_dev_barrier: sync, then (rank mode) an all-reduce every rank joins."""
+        _check(_lib().life_dev_barrier(self._h), "barrier")
 
     def layout(self, local_shard: int = 0) -> Layout:
         L = Layout()

@@ -1,0 +1,89 @@
+"""The driver's launcher support (driver/bootstrap.c), on the CPU: rank
+variables of torchrun / MPICH / Open MPI are recognised, and the 128-byte
+RCCL unique id travels from rank 0 to every other rank over TCP.  A small C
+harness links bootstrap.c alone (no HIP)."""
+import os
+import socket
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DRV = os.path.join(ROOT, "mpi-and-open-mp_amd", "driver")
+
+HARNESS = r"""
+#include <stdio.h>
+#include <string.h>
+#include "bootstrap.h"
+int main(void) {
+    int rank, world, local;
+    const int found = life_launcher_ranks(&rank, &world, &local);
+    if (found != 1) { printf("found %d\n", found); return 0; }
+    uint8_t id[LIFE_UID_BYTES];
+    memset(id, 0, sizeof id);
+    if (rank == 0) for (int k = 0; k < LIFE_UID_BYTES; k++) id[k] = (uint8_t)(k * 7 + 3);
+    const int rc = life_bootstrap_id(rank, world, id, 20.0);
+    printf("rank %d world %d local %d rc %d id", rank, world, local, rc);
+    for (int k = 0; k < LIFE_UID_BYTES; k += 16) printf(" %02x", id[k]);
+    printf("\n");
+    return rc ? 1 : 0;
+}
+"""
+
+
+@pytest.fixture(scope="module")
+def harness(tmp_path_factory):
+    d = tmp_path_factory.mktemp("boot")
+    (d / "h.c").write_text(HARNESS)
+    exe = d / "h"
+    subprocess.run(["gcc", "-O1", "-Wall", f"-I{DRV}", str(d / "h.c"), os.path.join(DRV, "bootstrap.c"), "-o",
+                    str(exe)], check=True)
+    return str(exe)
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def clean_env(**kv):
+    env = {k: v for k, v in os.environ.items()
+           if not k.startswith(("RANK", "WORLD_SIZE", "LOCAL_RANK", "PMI_", "OMPI_", "MPI_LOCALRANKID",
+                                "MASTER_", "LIFE_BOOTSTRAP"))}
+    env.update({k: str(v) for k, v in kv.items()})
+    return env
+
+
+@pytest.mark.parametrize("style", ["torchrun", "mpich", "openmpi"])
+def test_id_reaches_every_rank(harness, style):
+    world, port = 4, free_port()
+    names = {"torchrun": ("RANK", "WORLD_SIZE", "LOCAL_RANK"), "mpich": ("PMI_RANK", "PMI_SIZE", "MPI_LOCALRANKID"),
+             "openmpi": ("OMPI_COMM_WORLD_RANK", "OMPI_COMM_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_RANK")}[style]
+    procs = []
+    for r in (3, 1, 2, 0):  # rank 0 last: the others retry until it listens
+        env = clean_env(**{names[0]: r, names[1]: world, names[2]: r}, LIFE_BOOTSTRAP_PORT=port)
+        procs.append(subprocess.Popen([harness], env=env, stdout=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=60)[0] for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs
+    ids = {o.split(" id ")[1].strip() for o in outs}
+    assert len(ids) == 1 and ids.pop().startswith("03 73")  # id[0] = 3, id[16] = 115 from rank 0
+    assert sorted(int(o.split()[1]) for o in outs) == [0, 1, 2, 3]
+
+
+def test_no_launcher_and_bad_values(harness):
+    r = subprocess.run([harness], env=clean_env(), capture_output=True, text=True, timeout=30)
+    assert r.stdout.strip() == "found 0"
+    r = subprocess.run([harness], env=clean_env(RANK=4, WORLD_SIZE=4), capture_output=True, text=True, timeout=30)
+    assert r.stdout.strip() == "found -1"
+
+
+def test_master_port_plus_one(harness):
+    """torchrun's MASTER_ADDR / MASTER_PORT: the id goes over MASTER_PORT + 1."""
+    port = free_port()
+    procs = [subprocess.Popen([harness], env=clean_env(RANK=r, WORLD_SIZE=2, MASTER_ADDR="127.0.0.1",
+                                                         MASTER_PORT=port - 1), stdout=subprocess.PIPE, text=True)
+             for r in (1, 0)]
+    outs = [p.communicate(timeout=60)[0] for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs
+    assert outs[0].split(" id ")[1] == outs[1].split(" id ")[1]

@@ -98,7 +98,9 @@ def test_driver_p46gun_big(gpu, tmp_path):
 
 def test_driver_bits_frames_and_resume(gpu, tmp_path):
     """--format bits writes packed frames equal to the reference's frames;
-    --resume from generation 40 continues the reference's frame sequence."""
+    --resume from generation 40 continues the reference's frame sequence:
+    generations and frame numbers are absolute (--steps 100 ends where the
+    uninterrupted run ends, the first resumed frame is life_000040)."""
     frames = G["patterns"]["glider_10x10"]["frames"]
     r = subprocess.run([DRIVER, os.path.join(GOLDEN, "cfg", "glider_10x10.cfg"), "--format", "bits"], cwd=tmp_path,
                        capture_output=True, text=True, timeout=120)
@@ -108,11 +110,51 @@ def test_driver_bits_frames_and_resume(gpu, tmp_path):
         assert gen == i and md5(gpu.vtk_bytes(g)) == frames[str(i)][0], i
     run2 = tmp_path / "resumed"
     run2.mkdir()
-    r = subprocess.run([DRIVER, "--resume", str(tmp_path / "vtk" / "life_000040.bits"), "--steps", "60",
+    r = subprocess.run([DRIVER, "--resume", str(tmp_path / "vtk" / "life_000040.bits"), "--steps", "100",
                         "--save-steps", "10"], cwd=run2, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
-    for i in range(0, 60, 10):
-        assert md5((run2 / "vtk" / f"life_{i:06d}.vtk").read_bytes()) == frames[str(40 + i)][0], i
+    assert sorted(os.listdir(run2 / "vtk")) == [f"life_{i:06d}.vtk" for i in range(40, 100, 10)]
+    for i in range(40, 100, 10):
+        assert md5((run2 / "vtk" / f"life_{i:06d}.vtk").read_bytes()) == frames[str(i)][0], i
+
+
+LAUNCH_VARS = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "PMI_RANK", "PMI_SIZE", "OMPI_COMM_WORLD_RANK",
+               "OMPI_COMM_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+
+
+@pytest.mark.parametrize("launch", [{"RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0"},
+                                    {"PMI_RANK": "0", "PMI_SIZE": "1"},
+                                    {"OMPI_COMM_WORLD_RANK": "0", "OMPI_COMM_WORLD_SIZE": "1"}, "--rank-mode"],
+                         ids=["torchrun", "mpich", "openmpi", "flag"])
+def test_driver_rank_mode_glider(gpu, tmp_path, launch):
+    """Under a launcher the driver runs one-process-per-GPU (life_dev_create_rank,
+    an RCCL communicator, the root rank writes the frames): at world 1 the
+    frames are the reference's, byte for byte."""
+    env = {k: v for k, v in os.environ.items() if k not in LAUNCH_VARS}
+    args = [DRIVER, os.path.join(GOLDEN, "cfg", "glider_10x10.cfg")]
+    if isinstance(launch, dict):
+        env.update(launch)
+    else:
+        args.append(launch)
+    r = subprocess.run(args, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert len(r.stdout.splitlines()) == 1
+    frames = G["patterns"]["glider_10x10"]["frames"]
+    for i in range(100):
+        assert md5((tmp_path / "vtk" / f"life_{i:06d}.vtk").read_bytes()) == frames[str(i)][0], i
+
+
+def test_driver_refuses_gpus_under_launcher(gpu, tmp_path):
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1")
+    r = subprocess.run([DRIVER, os.path.join(GOLDEN, "cfg", "glider_10x10.cfg"), "--gpus", "2"], cwd=tmp_path,
+                       env=env, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "under a launcher" in r.stderr
+
+
+def test_driver_random_density_checked(gpu, tmp_path):
+    r = subprocess.run([DRIVER, "--random", "1,-0.5", "--nx", "64", "--ny", "64", "--steps", "2"], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "density" in r.stderr
 
 
 @pytest.mark.parametrize("kernel", ["byte", "bit"])

@@ -184,3 +184,42 @@ def test_bits_frame_roundtrip(lm, oracle, tmp_path):
     assert gen == 123
     np.testing.assert_array_equal(back, g)
     assert p.read_bytes().startswith(b"LIFEBITS 1 37 11 123\n") and len(p.read_bytes()) == 21 + 5 * 11
+
+
+def test_torch_after_library_is_refused(tmp_path):
+    """torch imported AFTER liblife_mi355x.so would map a second
+    HIP runtime (double free at exit): the binding refuses it with a clear
+    ImportError; torch first, then the library, is fine."""
+    import subprocess
+    import sys
+
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mpi-and-open-mp_amd")
+    bad = ("import sys; sys.path.insert(0, %r); import life_mi355x as lm; lm._lib()\n"
+           "try:\n    import torch\nexcept ImportError as e:\n    print('refused:', e)\n") % pkg
+    r = subprocess.run([sys.executable, "-c", bad], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "refused:" in r.stdout and "second copy" in r.stdout, r.stdout + r.stderr
+    good = ("import sys; sys.path.insert(0, %r); import torch; import life_mi355x as lm; lm._lib(); "
+            "print(lm.dims_create(8))") % pkg
+    r = subprocess.run([sys.executable, "-c", good], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "(4, 2)" in r.stdout, r.stdout + r.stderr
+
+
+def test_plot_life_against_gpu_count(tmp_path):
+    """scripts/plot_life.py (6-cartesian/plot_life.py:4-17): T1/TN against the
+    GPU count of each line (times.gpus beside times.txt, or --counts), else the
+    reference's 1..N ranks."""
+    import subprocess
+    import sys
+
+    script = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts", "plot_life.py")
+    (tmp_path / "times.txt").write_text("8.0\n4.1\n2.2\n1.25\n")
+    (tmp_path / "times.gpus").write_text("1\n2\n4\n8\n")
+    r = subprocess.run([sys.executable, script, "times.txt", "out.png"], cwd=tmp_path, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "8 GPU(s): 1.250000 s  speed-up 6.40  efficiency 0.80" in r.stdout
+    assert (tmp_path / "out.png").stat().st_size > 1000
+    (tmp_path / "times.gpus").unlink()
+    r = subprocess.run([sys.executable, script, "times.txt", "out2.png"], cwd=tmp_path, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0 and "4 GPU(s): 1.250000 s" in r.stdout  # reference convention: line k = k ranks
