@@ -90,6 +90,10 @@ def parse():
                    help="temporally blocked kernel: the tiled tstep_kernel (default) or sweep_kernel")
     p.add_argument("--rank-mode", action="store_true",
                    help="one-process-per-GPU set-up (gloo bootstrap, RCCL communicator) even at world 1")
+    p.add_argument("--loopback", action="store_true",
+                   help="N = 1: run the single grid as a periodic partition of itself (LIFE_OPT_LOOPBACK): the "
+                        "halo exchange, ring / interior overlap and (with --rank-mode) RCCL send/recv of the "
+                        "multi-GPU path, the shard its own neighbour")
     return p.parse_args()
 
 
@@ -218,6 +222,10 @@ def main():
 
     life = make_life(a, nx, ny, dims, rank_mode, dist, rank, world, local_rank)
     init_grid(life, a, grid)
+    if a.loopback:
+        if n_gpus != 1:
+            raise SystemExit("--loopback is a one-GPU mode")
+        life.configure(lm.OPT_LOOPBACK, 1)
     life.step(a.warmup)
     life.sync()
 
@@ -317,11 +325,11 @@ def main():
                                       + (" (one process per GPU, RCCL)" if rank_mode else
                                          f" ({life.world()['nlocal']} shards in one process, "
                                          f"{['auto', 'RCCL', 'LOCAL'][life.world()['transport']]} transport)"),
-                       "partition": partition, "temporal_kernel": a.temporal if temporal else "one-generation",
+                       "partition": partition + (" + loopback (the shard its own neighbour)" if a.loopback else ""), "temporal_kernel": a.temporal if temporal else "one-generation",
                        "generations_per_exchange": lay.generations_per_exchange, "live_cells_end": live},
             "roofline": roofline,
         }
-        if n_gpus > 1:
+        if n_gpus > 1 or a.loopback:
             out["phases"] = {"ring_ms": round(ph["ring_ms"], 4), "interior_ms": round(ph["interior_ms"], 4),
                              "halo_ms": round(ph["halo_ms"], 4), "block_ms": round(ph["block_ms"], 4),
                              "blocks": ph["blocks"], "exposed_ms": round(ph["block_ms"] - ph["interior_ms"], 4),

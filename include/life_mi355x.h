@@ -245,6 +245,26 @@ int life_dev_set_timing(life_dev *d, int on);
  * not fit run as value 1 without the window.  Value 4: as 1, never
  * windowed (the one-workgroup kernel; tests). */
 #define LIFE_OPT_SMALL_WINDOW 4
+/* LIFE_OPT_LOOPBACK (default 0; single-shard devices only): 1 runs the one
+ * shard as a periodic Cartesian partition of itself -- both axes' halos are
+ * exchanged through the transport with the shard as its own left and right
+ * neighbour (two sends and two receives to one peer per phase, as at
+ * dims = 2), the boundary ring and interior overlapped on their streams,
+ * instead of the stencil wrapping the axes.  With a rank-mode device
+ * (life_dev_create_rank, world 1, a unique id) the messages are RCCL
+ * ncclSend/ncclRecv: how one GPU executes the multi-GPU data path.  Results
+ * are identical either way.  The grid must be at least one halo deep
+ * (generations_per_exchange rows). */
+#define LIFE_OPT_LOOPBACK 6
+/* LIFE_OPT_FLOW (default 0, or LIFE_FLOW from the environment): a step call
+ * on a single shard whose axes both wrap inside it (bit encoding, width a
+ * multiple of 32) runs its whole passes of m generations (m = the block
+ * size, LIFE_OPT_BLOCK_GENS) as ONE persistent launch: workgroups pull
+ * (pass, tile) items in order and a tile starts when the tiles its window
+ * reads have finished the previous pass, so no pass boundary drains the chip;
+ * the remainder runs as an ordinary launch.  1: write-through hand-off
+ * stores; 2: plain stores + a release fence per tile.  Same results. */
+#define LIFE_OPT_FLOW 7
 int life_dev_configure(life_dev *d, int option, int value);
 int life_dev_kernel_stats(life_dev *d, double *avg_ms, int64_t *launches, double *bytes_per_launch);
 /* The same timed launches: mean cell-updates per launch (cells x generations

@@ -19,6 +19,11 @@ inline int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 inline int cart_rank(int c0, int c1, int dims1) { return c0 * dims1 + c1; }
 }  // namespace
 
+namespace life {
+int halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int kernel, bool loop, life_halo_op *ops,
+              int max_ops);
+}
+
 extern "C" {
 
 void life_decomposition(int64_t n, int p, int k, int64_t *start, int64_t *stop) {
@@ -129,8 +134,13 @@ int life_layout_query(int64_t nx, int64_t ny, int dims0, int dims1, int rank, in
     return LIFE_OK;
 }
 
-int life_halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int kernel,
-                   life_halo_op *ops, int max_ops) {
+}  // extern "C"
+
+// The halo plan; `loop` treats an axis the shard spans whole (dims == 1) as
+// partitioned too, with the shard as its own left and right neighbour
+// (LIFE_OPT_LOOPBACK: the transport's send/recv path exercised by one rank).
+int life::halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int kernel, bool loop,
+                    life_halo_op *ops, int max_ops) {
     life_layout L;
     const int rc = life_layout_query(nx, ny, dims0, dims1, rank, kernel, &L);
     if (rc != LIFE_OK) return rc;
@@ -151,7 +161,7 @@ int life_halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int k
         o.count = count;
     };
     // Phase 0: columns (dim 0 splits x), owned rows only.  MPI_Cart_shift(dim 0).
-    if (dims0 == 1) {
+    if (dims0 == 1 && !loop) {
         add(0, LIFE_HALO_FILL, -1, LIFE_HALO_COLUMN, -xa, xa, ya, h);
     } else {
         const int right = cart_rank((c0 + 1) % dims0, c1, dims1);
@@ -163,7 +173,7 @@ int life_halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int k
         add(0, LIFE_HALO_RECV, right, LIFE_HALO_COLUMN, w, xa, ya, h);
     }
     // Phase 1: whole rows including the x-apron just received (the corners).
-    if (dims1 == 1) {
+    if (dims1 == 1 && !loop) {
         add(1, LIFE_HALO_FILL, -1, LIFE_HALO_ROW, 0, ya, -xa, w + 2 * xa);
     } else {
         const int right = cart_rank(c0, (c1 + 1) % dims1, dims1);
@@ -179,6 +189,13 @@ int life_halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int k
         memcpy(ops, tmp, sizeof(life_halo_op) * n);
     }
     return n;
+}
+
+extern "C" {
+
+int life_halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int kernel,
+                   life_halo_op *ops, int max_ops) {
+    return life::halo_plan(nx, ny, dims0, dims1, rank, kernel, false, ops, max_ops);
 }
 
 const char *life_strerror(int err) {

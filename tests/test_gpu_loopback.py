@@ -1,0 +1,89 @@
+"""The multi-GPU halo data path executed on one GPU (LIFE_OPT_LOOPBACK).
+
+A single shard configured as a periodic Cartesian partition of itself: both
+axes' aprons come from halo messages the shard sends to itself (two sends
+and two receives to ONE peer per phase, matched in order -- the dims = 2 case
+of life_cart.c:225-279), with the boundary ring, the halo on the comm stream
+and the interior on the second compute stream overlapped as on N GPUs.  Over
+a rank-mode device (life_dev_create_rank, world 1, a unique id) the messages
+are RCCL ncclSend/ncclRecv: the RCCL branch of the exchange, its message
+sizes, group semantics and pack/unpack run here on the one-GPU box.  The
+bar is bit-exact against the oracle (3-life/life2d.c:104-130 restated) and
+against the same grid stepped without the loopback.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+# nx, ny, generations: temporal bit/byte layouts with whole and partial
+# words, several halo periods and a partial one; one-generation layouts
+# (w < 32); a grid exactly one halo deep
+CASES = [(256, 130, 45), (257, 131, 37), (512, 300, 70), (300, 64, 33), (31, 100, 9), (64, 32, 40), (1000, 37, 5)]
+
+
+def _make(gpu, nx, ny, kernel, rccl):
+    if rccl:
+        return gpu.Life.for_rank(nx, ny, 0, 1, gpu.unique_id(), 0, kernel=kernel)
+    return gpu.Life(nx, ny, kernel=kernel)
+
+
+@pytest.mark.parametrize("rccl", [False, True], ids=["local", "rccl"])
+@pytest.mark.parametrize("kernel", ["bit", "byte"])
+@pytest.mark.parametrize("nx,ny,gens", CASES)
+def test_loopback_parity(gpu, oracle, nx, ny, gens, kernel, rccl):
+    g0 = oracle.fill_random(nx, ny, seed=11, density=0.4)
+    want = oracle.life_run(g0, gens)
+    with _make(gpu, nx, ny, kernel, rccl) as life:
+        if life.layout().h < life.layout().generations_per_exchange:
+            with pytest.raises(RuntimeError):
+                life.configure(gpu.OPT_LOOPBACK, 1)
+            return
+        life.upload(g0)
+        life.configure(gpu.OPT_LOOPBACK, 1)
+        split = gens // 3
+        life.step(split)  # two calls: the schedule is re-entered mid-run
+        life.step(gens - split)
+        np.testing.assert_array_equal(life.gather(), want)
+        assert life.live_count() == int(want.sum())
+
+
+@pytest.mark.parametrize("kernel", ["bit", "byte"])
+def test_loopback_no_overlap_and_toggle(gpu, oracle, kernel):
+    """Serial schedule (overlap off), and loopback switched on and off
+    between step calls: the aprons are refilled from the shard each time."""
+    nx, ny = 320, 200
+    g0 = oracle.fill_random(nx, ny, seed=3, density=0.5)
+    with gpu.Life(nx, ny, kernel=kernel, overlap=False) as life:
+        life.upload(g0)
+        life.configure(gpu.OPT_LOOPBACK, 1)
+        life.step(21)
+        life.configure(gpu.OPT_LOOPBACK, 0)
+        life.step(13)
+        life.configure(gpu.OPT_LOOPBACK, 1)
+        life.step(40)
+        np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, 74))
+
+
+def test_loopback_rejected_for_partitioned(gpu):
+    with gpu.Life(512, 512, shards=2, kernel="bit", transport=gpu.XPORT_LOCAL) as life:
+        with pytest.raises(RuntimeError):
+            life.configure(gpu.OPT_LOOPBACK, 1)
+
+
+@pytest.mark.parametrize("kernel", ["bit", "byte"])
+def test_loopback_rccl_8192(gpu, kernel):
+    """8192^2 over RCCL loopback == the wrapped single shard (census checksum
+    and live count after several halo periods and a partial one)."""
+    n = 8192
+    with gpu.Life(n, n, kernel=kernel) as ref:
+        ref.fill_random(9, 0.5)
+        K = ref.layout().generations_per_exchange
+        gens = 3 * K + 5
+        ref.step(gens)
+        want = (ref.checksum(), ref.live_count())
+    with gpu.Life.for_rank(n, n, 0, 1, gpu.unique_id(), 0, kernel=kernel) as life:
+        life.fill_random(9, 0.5)
+        life.configure(gpu.OPT_LOOPBACK, 1)
+        life.step(gens)
+        assert (life.checksum(), life.live_count()) == want
