@@ -90,6 +90,9 @@ def parse():
                    help="temporally blocked kernel: the tiled tstep_kernel (default) or sweep_kernel")
     p.add_argument("--rank-mode", action="store_true",
                    help="one-process-per-GPU set-up (gloo bootstrap, RCCL communicator) even at world 1")
+    p.add_argument("--flow", type=int, default=None, choices=[0, 1, 2],
+                   help="LIFE_OPT_FLOW: single-shard bit tiles as one persistent dataflow launch per step call "
+                        "(1 write-through, 2 fenced hand-off; 0 per-launch tiles; default: the library's)")
     p.add_argument("--loopback", action="store_true",
                    help="N = 1: run the single grid as a periodic partition of itself (LIFE_OPT_LOOPBACK): the "
                         "halo exchange, ring / interior overlap and (with --rank-mode) RCCL send/recv of the "
@@ -147,6 +150,8 @@ def make_life(a, nx, ny, dims, rank_mode, dist, rank, world, local_rank):
         life = lm.Life(nx, ny, shards=a.gpus, kernel=a.kernel, dims=dims)
     if a.temporal == "sweep":
         life.configure(lm.OPT_SWEEP, 1)
+    if a.flow is not None:
+        life.configure(lm.OPT_FLOW, a.flow)
     return life
 
 

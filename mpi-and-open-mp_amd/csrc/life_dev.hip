@@ -93,6 +93,9 @@ struct Shard {
     uint8_t *sink = nullptr;  // stencil stores of lanes outside a region
     uint8_t *stage = nullptr;  // gather staging (grows on demand)
     size_t stage_bytes = 0;
+    unsigned int *flow = nullptr;  // dataflow tiles: queue head, error word, per-tile pass counts (grows on demand)
+    size_t flow_words = 0;
+    bool flow_used = false;  // a dataflow launch since the last sync checked its error word
     std::vector<life_halo_op> plan;
     std::vector<TimedLaunch> timers;
     size_t timers_used = 0;
@@ -114,6 +117,12 @@ static const int kEnvBlockGens = [] {
     const int v = e ? atoi(e) : 0;
     return v >= 1 && v <= 32 ? v : 0;
 }();
+// LIFE_FLOW (0/1/2) sets LIFE_OPT_FLOW's default at load time.
+static const int kEnvFlow = [] {
+    const char *e = getenv("LIFE_FLOW");
+    const int v = e ? atoi(e) : 0;
+    return v >= 0 && v <= 2 ? v : 0;
+}();
 static int default_block_gens(int kernel) {
     return kEnvBlockGens ? kEnvBlockGens : (kernel == LIFE_KERNEL_BIT ? 20 : 32);
 }
@@ -133,6 +142,9 @@ struct life_dev {
     int small_mode = 1;  // grids that fit one CU: 0 off, 1 VGPR kernel else LDS kernel, 2 LDS kernel,
                         // 3 windowed VGPR kernel over several CUs (else as 1), 4 as 1 never windowed
     int win_rows = 0, win_halo = 0;  // windowed kernel: strip height R, halo rows K (0: automatic)
+    bool loop = false;  // LIFE_OPT_LOOPBACK: the one shard exchanges both axes' halos with itself
+    int flow = kEnvFlow;  // LIFE_OPT_FLOW: single-shard bit tiles as one persistent dataflow launch per
+                          // step call (1: write-through hand-off, 2: plain stores + release; 0 off)
     std::vector<Shard> shards;
     double acc_ms = 0.0;
     int64_t acc_launches = 0;
@@ -146,9 +158,12 @@ struct life_dev {
 
 namespace {
 
+// Axis a's apron is filled by a halo exchange (dims[a] > 1, or the loopback
+// test mode, where the single shard is its own neighbour on both axes).
+bool part(const life_dev *d, int a) { return d->dims[a] > 1 || d->loop; }
 // The shard wraps x itself (the x-apron is filled by launch_wrap_columns).
-bool self_wrap_x(const life_dev *d) { return life::self_wrap_x(d->shards[0].lay, d->dims[0]); }
-life::Wrap wrap_of(const life_dev *d) { return life::Wrap{d->dims[0] == 1 && !self_wrap_x(d), d->dims[1] == 1}; }
+bool self_wrap_x(const life_dev *d) { return !d->loop && life::self_wrap_x(d->shards[0].lay, d->dims[0]); }
+life::Wrap wrap_of(const life_dev *d) { return life::Wrap{!part(d, 0) && !self_wrap_x(d), !part(d, 1)}; }
 
 int shard_alloc(life_dev *d, Shard &s) {
     HIPCHK(hipSetDevice(s.device));
@@ -174,7 +189,7 @@ int shard_alloc(life_dev *d, Shard &s) {
     HIPCHK(hipMalloc(&s.sink, 1024));
     HIPCHK(hipHostMalloc(&s.h_count, 2 * sizeof *s.h_count, hipHostMallocDefault));
     life_halo_op ops[16];
-    const int n = life_halo_plan(d->nx, d->ny, d->dims[0], d->dims[1], s.rank, d->kernel, ops, 16);
+    const int n = life::halo_plan(d->nx, d->ny, d->dims[0], d->dims[1], s.rank, d->kernel, d->loop, ops, 16);
     if (n < 0) {
         set_err("halo plan failed for shard %d", s.rank);
         return LIFE_EINVAL;
@@ -195,6 +210,7 @@ void shard_free(Shard &s) {
             if (e) (void)hipEventDestroy(e);
     for (uint8_t *p : {s.buf[0], s.buf[1], s.col_send, s.col_recv, s.sink, s.stage})
         if (p) (void)hipFree(p);
+    if (s.flow) (void)hipFree(s.flow);
     if (s.d_count) (void)hipFree(s.d_count);
     if (s.h_count) (void)hipHostFree(s.h_count);
     for (hipEvent_t e : {s.ev_ring, s.ev_halo, s.ev_sync, s.ev_int, s.ev_join, s.ev_entry})
@@ -244,11 +260,11 @@ void op_buffer(const Shard &s, const life_halo_op &o, int slot, uint8_t *base, u
 int run_phase(life_dev *d, int phase, int which_rel, bool on_comm) {
     auto stream_of = [&](Shard &s) { return on_comm ? s.comm_stream : s.stream; };
     auto buf_of = [&](Shard &s) { return s.buf[s.cur ^ which_rel]; };
-    // An axis that is not partitioned (dims[d] == 1) has no halo: the stencil
+    // An axis that is not partitioned (dims[d] == 1, no loopback) has no halo: the stencil
     // wraps it itself (life_kernels.hip, row_ptr / WRAPX), or, for a temporal
     // layout whose width is not a multiple of 32, the shard copies its own
     // edge columns into its x-apron.
-    if (d->dims[phase] == 1) {
+    if (!part(d, phase)) {
         if (phase == 0 && self_wrap_x(d))
             for (Shard &s : d->shards) {
                 HIPCHK(hipSetDevice(s.device));
@@ -584,7 +600,7 @@ int next_block(const life_dev *d, int64_t remaining) {
 // [w-32, w).  A self-wrapped x axis (life::self_wrap_x) counts as
 // partitioned: its "exchange" is the column copy.
 int generation_block(life_dev *d, int m) {
-    const bool rx = d->dims[0] > 1 || self_wrap_x(d), ry = d->dims[1] > 1;
+    const bool rx = part(d, 0) || self_wrap_x(d), ry = part(d, 1);
     std::vector<PhaseEvents *> pe(d->shards.size(), nullptr);
     for (size_t si = 0; si < d->shards.size(); ++si) {
         Shard &s = d->shards[si];
@@ -659,7 +675,7 @@ int generation_block(life_dev *d, int m) {
 
 // One generation on every local shard (one-cell aprons).
 int generation(life_dev *d) {
-    const bool rx = d->dims[0] > 1, ry = d->dims[1] > 1;
+    const bool rx = part(d, 0), ry = part(d, 1);
     if (!d->overlap || !(rx || ry)) {
         for (Shard &s : d->shards) {
             HIPCHK(hipSetDevice(s.device));
@@ -890,7 +906,7 @@ static life::RegWinPlan win_plan(const life_dev *d) {
 }
 
 static bool small_grid(const life_dev *d) {
-    if (d->world != 1 || d->shards.size() != 1 || d->small_mode == 0) return false;
+    if (d->world != 1 || d->shards.size() != 1 || d->small_mode == 0 || d->loop) return false;
     const life_layout &L = d->shards[0].lay;
     if (win_plan(d).blocks > 0) return true;
     return (d->small_mode != 2 && life::reg_small_rows(L) > 0) ||
@@ -937,6 +953,58 @@ static int step_small(life_dev *d, int64_t generations) {
     return LIFE_OK;
 }
 
+// Whole passes of the dataflow tiles (life::launch_tflow) for a step call of
+// `generations` on a single shard whose axes both wrap in the stencil;
+// returns the generations it queued (a multiple of the pass size m), 0 when
+// the call takes the per-launch path.
+static int step_flow(life_dev *d, int64_t generations, int64_t *done) {
+    *done = 0;
+    if (!d->flow || d->sweep || d->shards.size() != 1 || d->world != 1 || d->kernel != LIFE_KERNEL_BIT ||
+        part(d, 0) || part(d, 1) || self_wrap_x(d))
+        return LIFE_OK;
+    Shard &s = d->shards[0];
+    const life_layout &L = s.lay;
+    int m = std::min(L.generations_per_exchange, 32);
+    if (d->block_gens > 0) m = std::min(m, d->block_gens);
+    const int64_t passes = generations / m;
+    if (passes < 2 || !life::flow_ok(L, m)) return LIFE_OK;
+    const life::TileGeom g = life::tile_geom(L, m);
+    const size_t words = (size_t)(2 + g.ntx * g.nty);
+    if (words > s.flow_words) {
+        if (s.flow) (void)hipFree(s.flow);
+        s.flow = nullptr;
+        s.flow_words = 0;
+        if (hipSetDevice(s.device) != hipSuccess || hipMalloc(&s.flow, words * sizeof(unsigned int)) != hipSuccess ||
+            hipMemset(s.flow, 0, 2 * sizeof(unsigned int)) != hipSuccess) {
+            set_err("dataflow scratch (%zu words)", words);
+            return LIFE_ENOMEM;
+        }
+        s.flow_words = words;
+    }
+    HIPCHK(hipSetDevice(s.device));
+    TimedLaunch *t = nullptr;
+    if (d->timing) {
+        int rc;
+        t = timer_slot(s, &rc);
+        if (!t) return rc;
+        HIPCHK(hipEventRecord(t->a, s.stream));
+    }
+    HIPCHK(life::launch_tflow(L, s.buf[s.cur], s.buf[s.cur ^ 1], m, passes, s.flow, s.flow + 2, wrap_of(d),
+                                 d->flow, s.stream));
+    if (t) {
+        HIPCHK(hipEventRecord(t->b, s.stream));
+        t->launches = (int)passes;  // stats: mean per pass
+        const double cells = (double)L.w * (double)L.h;
+        d->acc_bytes += (double)passes * cells * 0.25;
+        d->acc_updates += (double)passes * cells * (double)m;
+        d->acc_valu += (double)passes * (double)(g.ntx * g.nty) * 64.0 * life::tstep_valu_per_tile_lane(m, false);
+    }
+    if (passes & 1) s.cur ^= 1;
+    s.flow_used = true;
+    *done = passes * m;
+    return LIFE_OK;
+}
+
 int life_dev_step(life_dev *d, int64_t generations) {
     if (!d || generations < 0) return LIFE_EINVAL;
     if (generations == 0) return LIFE_OK;
@@ -959,7 +1027,9 @@ int life_dev_step(life_dev *d, int64_t generations) {
         return exchange(d, 0, false);
     }
     if (temporal(d)) {
-        for (int64_t g = 0; g < generations;) {
+        int64_t done = 0;
+        CHK(step_flow(d, generations, &done));
+        for (int64_t g = done; g < generations;) {
             const int m = next_block(d, generations - g);
             CHK(generation_block(d, m));
             g += m;
@@ -1001,6 +1071,18 @@ int life_dev_sync(life_dev *d) {
         HIPCHK(hipStreamSynchronize(s.stream));
         HIPCHK(hipStreamSynchronize(s.stream2));
         HIPCHK(hipStreamSynchronize(s.comm_stream));
+        if (s.flow_used) {
+            // a dataflow launch whose dependency wait timed out (a broken
+            // hand-off): its result cannot be trusted
+            unsigned int err = 0;
+            HIPCHK(hipMemcpy(&err, s.flow + 1, sizeof err, hipMemcpyDeviceToHost));
+            s.flow_used = false;
+            if (err) {
+                HIPCHK(hipMemset(s.flow + 1, 0, sizeof err));
+                set_err("dataflow tiles: item %u waited too long for its neighbours (state is invalid)", err - 1);
+                return LIFE_ESTATE;
+            }
+        }
     }
     return LIFE_OK;
 }
@@ -1200,6 +1282,36 @@ int life_dev_configure(life_dev *d, int option, int value) {
         if (value < 0 || value > 1) return LIFE_EINVAL;
         d->sweep = value != 0;
         return LIFE_OK;
+    case LIFE_OPT_FLOW:
+        if (value < 0 || value > 2) return LIFE_EINVAL;
+        d->flow = value;
+        return LIFE_OK;
+    case LIFE_OPT_LOOPBACK: {
+        if (value < 0 || value > 1) return LIFE_EINVAL;
+        if (d->world != 1 || d->shards.size() != 1) {
+            set_err("loopback needs a single-shard world (world %d, %zu local shards)", d->world, d->shards.size());
+            return LIFE_EINVAL;
+        }
+        Shard &s = d->shards[0];
+        // the apron a partitioned y axis needs: at least K rows to send
+        if (value && s.lay.h < s.lay.yapron) {
+            set_err("loopback: %lld rows < the %lld-row halo", (long long)s.lay.h, (long long)s.lay.yapron);
+            return LIFE_EINVAL;
+        }
+        if (value && d->transport == LIFE_XPORT_RCCL && !s.comm) {
+            set_err("loopback over RCCL needs a communicator (life_dev_create_rank with a unique id)");
+            return LIFE_EINVAL;
+        }
+        // the current state's aprons are refreshed on the next step's first
+        // exchange only: fill them now from the shard itself
+        d->loop = value != 0;
+        life_halo_op ops[16];
+        const int n = life::halo_plan(d->nx, d->ny, d->dims[0], d->dims[1], s.rank, d->kernel, d->loop, ops, 16);
+        if (n < 0) return LIFE_EINVAL;
+        s.plan.assign(ops, ops + n);
+        CHK(exchange(d, 0, false));
+        return life_dev_sync(d);
+    }
     default: return LIFE_EINVAL;
     }
 }

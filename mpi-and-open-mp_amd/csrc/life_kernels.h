@@ -64,6 +64,19 @@ int tile_ghost(const life_layout &L, int m);  // ghost rows per window end: m (b
 // the last tile's window (<= 8 waves x 96 rows) may read past the bottom
 // apron without clamping.
 constexpr int64_t kTemporalSlackRows = 8 * 96;
+// Dataflow form of the bit tiles (tflow_kernel): `passes` launches of m
+// generations over a single shard whose axes both wrap inside it, as ONE
+// persistent launch (no drain between passes).  `head` (2 words: the queue
+// head, then an error word the caller zeroes once and reads: 1 + an item
+// whose dependency wait timed out, 0 if none) and `done`
+// (ntx * nty words, tile_geom(L, m)) are device scratch the launch zeroes;
+// flow 1: write-through (`sc1`) stores, 2: plain stores + release fence.
+// Pass p reads `in` for even p and `out` for odd p: after it, the result is
+// in `out` when passes is odd, else in `in`.
+bool flow_ok(const life_layout &L, int m);
+int flow_slots();  // resident workgroups of the dataflow kernel on this device
+hipError_t launch_tflow(const life_layout &L, const uint8_t *in, uint8_t *out, int m, int64_t passes,
+                        unsigned int *head, unsigned int *done, Wrap wrap, int flow, hipStream_t s);
 // Up to 4 disjoint tile regions in one launch.
 hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, const TileRegion *r, int nreg,
                         int m, Wrap wrap, hipStream_t s);
@@ -136,6 +149,11 @@ inline bool self_wrap_x(const life_layout &L, int dims0) {
     return L.xapron == 32 && dims0 == 1 && L.w % 32 != 0;
 }
 hipError_t launch_wrap_columns(const life_layout &L, uint8_t *buf, hipStream_t s);
+
+// life_halo_plan with `loop`: an axis with dims == 1 is exchanged too, the
+// shard being its own neighbour (life_plan.cpp; LIFE_OPT_LOOPBACK).
+int halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int kernel, bool loop, life_halo_op *ops,
+              int max_ops);
 
 // Dense w*h byte block (row pitch w) <-> padded encoded buffer.
 hipError_t launch_import_block(const life_layout &L, const uint8_t *dense, uint8_t *buf,

@@ -293,9 +293,18 @@ __device__ __forceinline__ void bit_hsum(uint32_t v, uint32_t &s0, uint32_t &s1)
 // <= 32 bits after K generations), so rows [K, K+T) of lanes 1..62 are exact.
 // Bit: centred frame (bit_hsum); byte: drifting frame (bit_hsum_drift; +2 %
 // there, -1 % for bit: profiles/r01/drift_ab.jsonl).
-template <bool BYTE, int R, int GK, bool WRAPX, bool WRAPY>
-__global__ __launch_bounds__(64 * kStackWaves, 4) void tstep_kernel(TArgs a) {  // 4 waves/SIMD: 2 tiles per CU
+//
+// FLOW (tflow_kernel, bit only): the window is loaded with agent-scope
+// (`sc1`, L1-bypassing) loads, and stored with `sc1` write-through stores
+// (FLOW 1) or plain stores (FLOW 2, the kernel releases them with a fence):
+// the rows are another workgroup's output of the same launch.
+using Xch = uint32_t[2][kStackWaves][4][64];  // [parity][wave][top s0/s1, bottom s0/s1][lane]
+
+template <bool BYTE, int R, int GK, bool WRAPX, bool WRAPY, int FLOW>
+__device__ __forceinline__ void tile_body(const TArgs &a, const uint8_t *in, uint8_t *out, int64_t tx, int64_t ty,
+                                          Xch &xch) {
     static_assert(R >= 3 && GK >= 0 && GK <= 32, "window");
+    static_assert(FLOW == 0 || !BYTE, "dataflow tiles: bit encoding");
     constexpr int NW = kStackWaves;
     // the window's ghost rows at each end: GK, or (GK = 0) the launch's
     // generations m <= 32 (checked on the host); after m generations rows
@@ -304,20 +313,11 @@ __global__ __launch_bounds__(64 * kStackWaves, 4) void tstep_kernel(TArgs a) {  
     // ghost_ab.txt); the bit tiles run the same either way.
     const int K = GK > 0 ? GK : a.m;
     const int T = NW * R - 2 * K;
-    __shared__ uint32_t xch[2][NW][4][64];  // [parity][wave][top s0/s1, bottom s0/s1][lane]
     constexpr bool DRIFT = BYTE;
     const int lane = threadIdx.x & 63;
     const int laddr = ((lane - 1) & 63) << 2;
     // wave index: uniform, so every row address below is scalar (SALU) math
     const int wi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t nwg = a.first[a.nreg];
-    if ((int64_t)blockIdx.x >= nwg) return;  // whole workgroup
-    const int64_t wg = blockIdx.x;
-    int k = 0;
-    while (k + 1 < a.nreg && wg >= a.first[k + 1]) ++k;
-    const int64_t wr = wg - a.first[k];
-    const int64_t ntx = a.tx1[k] - a.tx0[k];
-    const int64_t tx = a.tx0[k] + wr % ntx, ty = a.ty0[k] + wr / ntx;
     const int64_t j = tx * 62 + lane - 1;  // word column of this lane
     int64_t jl;
     if (WRAPX) {
@@ -332,7 +332,7 @@ __global__ __launch_bounds__(64 * kStackWaves, 4) void tstep_kernel(TArgs a) {  
     // with an apron the last tile's window may run past the apron row h+K-1
     // into the allocation slack below the buffer (kTemporalSlackRows; those
     // rows are never stored).
-    const uint8_t *row0 = a.in + a.ya * a.pitch;  // owned row 0
+    const uint8_t *row0 = in + a.ya * a.pitch;  // owned row 0
     int64_t y = y0;
     if (WRAPY) {
         y %= a.h;
@@ -345,6 +345,9 @@ __global__ __launch_bounds__(64 * kStackWaves, 4) void tstep_kernel(TArgs a) {  
         if (BYTE) {
             const uint4 *q = reinterpret_cast<const uint4 *>(p + voff);
             v[r] = pack32(q[0], q[1]);
+        } else if (FLOW) {
+            v[r] = __hip_atomic_load(reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(p) + voff), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
         } else {
             v[r] = *reinterpret_cast<const uint32_t *>(p + voff);
         }
@@ -412,7 +415,7 @@ __global__ __launch_bounds__(64 * kStackWaves, 4) void tstep_kernel(TArgs a) {  
     const bool st = lane >= 1 && lane <= 62 && j < a.W;
     // window rows [K, NW*R - K) are the tile's owned rows [ty*T, ty*T + T)
     const int r0 = wi == 0 ? K : 0, r1 = wi == NW - 1 ? R - K : R;
-    uint8_t *q = a.out + (a.ya + y0 + r0) * a.pitch + voff;
+    uint8_t *q = out + (a.ya + y0 + r0) * a.pitch + voff;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         if (r < r0 || r >= r1) continue;
@@ -422,11 +425,125 @@ __global__ __launch_bounds__(64 * kStackWaves, 4) void tstep_kernel(TArgs a) {  
                 uint4 *o = reinterpret_cast<uint4 *>(q);
                 o[0] = unpack_half(v[r], 0);
                 o[1] = unpack_half(v[r], 1);
+            } else if (FLOW == 1) {
+                __hip_atomic_store(reinterpret_cast<uint32_t *>(q), v[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {
                 *reinterpret_cast<uint32_t *>(q) = v[r];
             }
         }
         q += a.pitch;
+    }
+}
+
+template <bool BYTE, int R, int GK, bool WRAPX, bool WRAPY>
+__global__ __launch_bounds__(64 * kStackWaves, 4) void tstep_kernel(TArgs a) {  // 4 waves/SIMD: 2 tiles per CU
+    __shared__ Xch xch;
+    const int64_t nwg = a.first[a.nreg];
+    if ((int64_t)blockIdx.x >= nwg) return;  // whole workgroup
+    const int64_t wg = blockIdx.x;
+    int k = 0;
+    while (k + 1 < a.nreg && wg >= a.first[k + 1]) ++k;
+    const int64_t wr = wg - a.first[k];
+    const int64_t ntx = a.tx1[k] - a.tx0[k];
+    const int64_t tx = a.tx0[k] + wr % ntx, ty = a.ty0[k] + wr / ntx;
+    tile_body<BYTE, R, GK, WRAPX, WRAPY, 0>(a, a.in, a.out, tx, ty, xch);
+}
+
+// tflow_kernel: `passes` launches of the bit tiles (m generations each, both
+// axes periodic inside one shard) as ONE persistent launch.  Workgroups pull
+// work items (pass p, tile) in order from a queue head; a tile of pass p > 0
+// starts once every tile whose rows its window reads -- tile rows ty-2..ty+2
+// (a short last tile row lets a window reach two rows over), columns
+// tx-1..tx+1, periodic -- has finished pass p-1, which also guarantees that no
+// reader of the rows it overwrites (pass p-1 of the same tiles) is still
+// running.  Pass p walks the tile rows from row p (mod nty), so the rows a
+// tile waits for were pulled about a whole pass earlier: no pass boundary
+// drains the chip (the per-launch ramp and tail of tstep_kernel, ~48 us).
+// Deadlock-free without co-residency: an item waits only on items pulled
+// before it, and a pulled item is running on a resident workgroup.
+// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, row 1): the
+// window rows are loaded `sc1`; every storing wave waits vmcnt(0), then a
+// workgroup barrier, then one lane stores the tile's pass count `sc1`; the
+// polling wave's lanes read the flags `sc1`, a barrier, then every wave loads.
+struct FArgs {
+    TArgs t;                         // geometry, m; t.in / t.out: buffers of pass 0
+    int64_t ntx, nty, items;         // items = passes * ntx * nty
+    unsigned int *head;              // queue head (zeroed before the launch), then an error word: 1 + the
+                                     // last item whose dependency wait timed out (0: none)
+    unsigned int *done;              // per tile: passes completed (zeroed before the launch)
+};
+
+template <int R, bool WRAPX, bool WRAPY, int FLOW>
+__global__ __launch_bounds__(64 * kStackWaves, 6) void tflow_kernel(FArgs f) {  // 3 tiles per CU
+    __shared__ Xch xch;
+    __shared__ unsigned int item_sh;
+    const TArgs &a = f.t;
+    const int64_t tiles = f.ntx * f.nty;
+    const int lane = threadIdx.x & 63;
+    unsigned int *prev_flag = nullptr;  // thread 0: the finished item's tile counter
+    unsigned int prev_val = 0;
+    for (;;) {
+        // ONE thread-0 region per iteration, behind the barrier that closes
+        // the previous item: publish that item (its stores were drained by
+        // every wave before the barrier), then pull the next.  (Two thread-0
+        // regions on either side of the loop's back edge were merged by the
+        // compiler into a region that lanes 1..63 of wave 0 never wait for:
+        // the workgroup then re-ran its item forever.)
+        if (threadIdx.x == 0) {
+            if (prev_flag) {
+                if (FLOW == 2) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                __hip_atomic_store(prev_flag, prev_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            item_sh = atomicAdd(f.head, 1u);
+        }
+        __syncthreads();
+        // uniform: scalar registers, scalar arithmetic
+        const uint32_t item = __builtin_amdgcn_readfirstlane(item_sh);
+        if ((int64_t)item >= f.items) return;  // the whole workgroup leaves
+        const uint32_t ntx = (uint32_t)f.ntx, nty = (uint32_t)f.nty;
+        const uint32_t p = item / (uint32_t)tiles, k = item - p * (uint32_t)tiles;
+        const uint32_t kr = k / ntx;
+        const int64_t tx = k - kr * ntx, ty = (kr + p) % nty;
+        if (p > 0 && threadIdx.x < 64) {
+            // 15 lanes: tile rows ty-2..ty+2 x columns tx-1..tx+1
+            bool ok = true;
+            const unsigned int *flag = nullptr;
+            if (lane < 15) {
+                const int64_t dy = lane / 3 - 2, dx = lane % 3 - 1;
+                int64_t yy = (ty + dy) % f.nty, xx = (tx + dx) % f.ntx;
+                if (yy < 0) yy += f.nty;
+                if (xx < 0) xx += f.ntx;
+                flag = f.done + yy * f.ntx + xx;
+            }
+            // bounded: a wait of ~seconds means a broken invariant; record it
+            // (the host reports it at the next sync) rather than hang the GPU
+            for (uint32_t spin = 0;; ++spin) {
+                if (flag)
+                    ok = __hip_atomic_load(const_cast<unsigned int *>(flag), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT) >= p;
+                if (__all(ok)) break;
+                if (spin == (1u << 20)) {
+                    if (lane == 0) atomicMax(f.head + 1, item + 1);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            if (FLOW == 2) {  // plain producer stores: the valid form needs the acquire
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        }
+        __syncthreads();
+        const uint8_t *in = (p & 1) ? a.out : a.in;
+        uint8_t *out = const_cast<uint8_t *>((p & 1) ? a.in : a.out);
+        tile_body<false, R, 0, WRAPX, WRAPY, FLOW>(a, in, out, tx, ty, xch);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
+        __syncthreads();
+        prev_flag = f.done + ty * f.ntx + tx;
+        prev_val = p + 1;
     }
 }
 
@@ -1106,6 +1223,13 @@ hipError_t launch_k(const TArgs &a, Wrap wrap, unsigned grid, hipStream_t s) {
 
 int tile_ghost(const life_layout &L, int m) { return is_bit(L) ? m : L.generations_per_exchange; }
 
+bool flow_ok(const life_layout &L, int m) {
+    // the dependency rule reads tile rows ty-2..ty+2: a window may reach at
+    // most one tile row beyond its neighbours (m <= T)
+    const TileGeom g = tile_geom(L, m);
+    return is_bit(L) && g.rows >= m && m >= 1;
+}
+
 TileGeom tile_geom(const life_layout &L, int m) {
     TileGeom g;
     g.words = 62;
@@ -1148,6 +1272,63 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
     const unsigned grid = (unsigned)a.first[a.nreg];  // one workgroup per tile
     if (is_bit(L)) return launch_k<false, 0>(a, wrap, grid, s);
     return K == 16 ? launch_k<true, 16>(a, wrap, grid, s) : launch_k<true, 32>(a, wrap, grid, s);
+}
+
+namespace {
+template <int R>
+hipError_t launch_fr(const FArgs &f, int flow, unsigned grid, hipStream_t s) {
+    constexpr unsigned kThreads = 64 * kStackWaves;
+    if (flow == 2)
+        tflow_kernel<R, true, true, 2><<<grid, kThreads, 0, s>>>(f);
+    else
+        tflow_kernel<R, true, true, 1><<<grid, kThreads, 0, s>>>(f);
+    return hipGetLastError();
+}
+}  // namespace
+
+int flow_slots() {
+    static const int slots = [] {
+        int dev = 0, cus = 0, per = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return 0;
+        const void *fn = temporal_rows(true) == 40 ? (const void *)tflow_kernel<40, true, true, 1>
+                                                   : (const void *)tflow_kernel<48, true, true, 1>;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 64 * kStackWaves, 0) != hipSuccess) return 0;
+        return cus * per;
+    }();
+    return slots;
+}
+
+hipError_t launch_tflow(const life_layout &L, const uint8_t *in, uint8_t *out, int m, int64_t passes,
+                        unsigned int *head, unsigned int *done, Wrap wrap, int flow, hipStream_t s) {
+    const int R = temporal_rows(true);
+    if (!is_bit(L) || !wrap.x || !wrap.y || m < 1 || m > 32 ||
+        m > L.generations_per_exchange || passes < 1 || (R != 40 && R != 48) || !flow_ok(L, m))
+        return hipErrorInvalidValue;
+    const TileGeom g = tile_geom(L, m);
+    FArgs f{};
+    f.t.in = in;
+    f.t.out = out;
+    f.t.pitch = L.pitch;
+    f.t.xoff = L.xoff;
+    f.t.W = (L.w + 31) / 32;
+    f.t.h = L.h;
+    f.t.ya = L.yapron;
+    f.t.m = m;
+    f.ntx = g.ntx;
+    f.nty = g.nty;
+    f.items = passes * g.ntx * g.nty;
+    f.head = head;
+    f.done = done;
+    if (f.items >= (int64_t)UINT32_MAX) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(head, 0, sizeof(unsigned int), s);  // the error word is the caller's
+    if (e == hipSuccess) e = hipMemsetAsync(done, 0, sizeof(unsigned int) * (size_t)(g.ntx * g.nty), s);
+    if (e != hipSuccess) return e;
+    const int slots = flow_slots();
+    if (slots <= 0) return hipErrorInvalidValue;
+    const unsigned grid = (unsigned)std::min<int64_t>(f.items, slots);
+    return R == 40 ? launch_fr<40>(f, flow, grid, s) : launch_fr<48>(f, flow, grid, s);
 }
 
 int reg_small_rows(const life_layout &L) {

@@ -1,0 +1,60 @@
+"""The dataflow form of the bit tiles (LIFE_OPT_FLOW): whole passes of a step
+call as ONE persistent launch whose workgroups pull (pass, tile) items and
+wait for the tiles their windows read (life_kernels.hip tflow_kernel).  The
+hand-off between workgroups (agent-scope loads, write-through or fenced
+stores, per-tile pass counters) is what can go wrong, so the bar is
+bit-exact against the oracle (3-life/life2d.c:104-130 restated) on shapes
+with full and partial tile rows / columns and a short last tile row, and
+census-equal to the per-launch tiles at sizes where many passes overlap on
+a loaded chip.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+# nx (multiple of 32: x wraps inside the words), ny, generations, m
+CASES = [(2048, 1000, 47, 20), (1024, 3000, 64, 16), (4096, 1100, 33, 10), (1984, 700, 90, 32), (64, 900, 25, 8),
+         (2080, 2000, 61, 12), (32, 2048, 40, 20)]
+
+
+@pytest.mark.parametrize("flow", [1, 2])
+@pytest.mark.parametrize("nx,ny,gens,m", CASES)
+def test_flow_parity(gpu, oracle, nx, ny, gens, m, flow):
+    g0 = oracle.fill_random(nx, ny, seed=21, density=0.45)
+    want = oracle.life_run(g0, gens)
+    with gpu.Life(nx, ny, kernel="bit", small_grid=False) as life:
+        life.configure(gpu.OPT_FLOW, flow)
+        life.configure(gpu.OPT_BLOCK_GENS, m)
+        life.upload(g0)
+        life.set_timing(True)
+        life.step(gens)
+        avg_ms, launches, _ = life.kernel_stats()
+        assert launches >= gens // m  # the passes were timed as one launch each
+        np.testing.assert_array_equal(life.gather(), want)
+        assert life.live_count() == int(want.sum())
+
+
+@pytest.mark.parametrize("flow", [1, 2])
+@pytest.mark.parametrize("n,m", [(16384, 20), (32768, 10), (65536, 16)])
+def test_flow_fullsize_census(gpu, n, m, flow):
+    """Many overlapped passes on a loaded chip: the census (checksum + live
+    count) equals the per-launch tiles' after the same generations."""
+    gens = 7 * m + 3
+    with gpu.Life(n, n, kernel="bit") as ref:
+        ref.configure(gpu.OPT_BLOCK_GENS, m)
+        ref.fill_random(5, 0.5)
+        ref.step(gens)
+        want = (ref.checksum(), ref.live_count())
+    with gpu.Life(n, n, kernel="bit") as life:
+        life.configure(gpu.OPT_FLOW, flow)
+        life.configure(gpu.OPT_BLOCK_GENS, m)
+        life.fill_random(5, 0.5)
+        life.step(gens)
+        assert (life.checksum(), life.live_count()) == want
+
+
+def test_flow_rejected_options(gpu):
+    with gpu.Life(256, 256, kernel="bit") as life:
+        with pytest.raises(RuntimeError):
+            life.configure(gpu.OPT_FLOW, 3)

@@ -197,3 +197,15 @@ def test_driver_large_cfg_parallel_parse(gpu, tmp_path):
     bad.write_text(head + "1 2\n3 x4\n")
     r = subprocess.run([DRIVER, str(bad)], cwd=tmp_path, capture_output=True, text=True, timeout=60)
     assert r.returncode == 1 and "cannot read config" in r.stderr
+
+
+@pytest.mark.parametrize("kernel", ["byte", "bit"])
+def test_gather_vtk_8192_four_shards(gpu, oracle, kernel):
+    """The device VTK formatter at scale: 8192^2 over 2x2 shards (life_cart.c's
+    gather-then-save path, :159-187) == the host formatting of the gathered
+    grid, byte for byte (134 MB of cell text)."""
+    n = 8192
+    with gpu.Life(n, n, shards=4, kernel=kernel, transport=gpu.XPORT_LOCAL) as life:
+        life.fill_random(77, 0.5)
+        life.step(37)
+        assert life.gather_vtk() == gpu.vtk_bytes(life.gather())
