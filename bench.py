@@ -86,8 +86,6 @@ def parse():
                    help="N > 1: the 1-GPU reference re-runs the timed generations when that is estimated to take "
                         "less than this, else a fresh 3K+1-generation run of both")
     p.add_argument("--no-parity", action="store_true")
-    p.add_argument("--temporal", default="tiles", choices=["sweep", "tiles"],
-                   help="temporally blocked kernel: the tiled tstep_kernel (default) or sweep_kernel")
     p.add_argument("--rank-mode", action="store_true",
                    help="one-process-per-GPU set-up (gloo bootstrap, RCCL communicator) even at world 1")
     p.add_argument("--flow", type=int, default=None, choices=[0, 1, 2],
@@ -148,8 +146,6 @@ def make_life(a, nx, ny, dims, rank_mode, dist, rank, world, local_rank):
         life = lm.Life.for_rank(nx, ny, rank, world, uid[0], local_rank, kernel=a.kernel, dims=dims)
     else:
         life = lm.Life(nx, ny, shards=a.gpus, kernel=a.kernel, dims=dims)
-    if a.temporal == "sweep":
-        life.configure(lm.OPT_SWEEP, 1)
     if a.flow is not None:
         life.configure(lm.OPT_FLOW, a.flow)
     return life
@@ -246,6 +242,7 @@ def main():
     barrier_sync()
     t0 = time.perf_counter()
     life.step(a.steps)
+    path = life.last_path()  # the kernel family of the timed call
     barrier_sync()
     elapsed = time.perf_counter() - t0
 
@@ -283,8 +280,8 @@ def main():
         hbm = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
         gens_per_launch = updates_per_launch / (bytes_per_launch / bpu) if bytes_per_launch > 0 else 0.0
         variant = a.kernel + ("_temporal" if temporal else "_onegen")
-        if temporal and a.temporal == "sweep":
-            variant += "_sweep"
+        if path == "flow" and a.kernel == "bit":
+            variant = "bit_flow"
         traffic = load_traffic(variant, a.size) if (a.workload == "random" and not strong) else None
         hbm_obj = {"achieved": round(hbm, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                    "frac": round(hbm / HBM_PEAK_GBS, 4),
@@ -305,8 +302,8 @@ def main():
                         "unit": "Tlane-op/s", "frac": round(tops / VALU_PEAK_TOPS, 4), "traffic": traffic,
                         "kernel_avg_ms": round(avg_ms, 5), "kernel_launches": launches,
                         "generations_per_launch": round(gens_per_launch, 3), "ops_per_launch": valu_per_launch,
-                        "model": "per register row and generation 13 VALU (tiles; byte: 12 + pack/unpack) or "
-                                 "12 per stage-step (sweep), life_kernels.hip / life_sweep.hip",
+                        "model": "per register row and generation 13 VALU (tiles; byte: 12 + pack/unpack), "
+                                 "life_kernels.hip tile_body",
                         "hbm": hbm_obj}
         else:
             roofline = dict(hbm_obj, bound="hbm", traffic=traffic, kernel_avg_ms=round(avg_ms, 5),
@@ -330,7 +327,7 @@ def main():
                                       + (" (one process per GPU, RCCL)" if rank_mode else
                                          f" ({life.world()['nlocal']} shards in one process, "
                                          f"{['auto', 'RCCL', 'LOCAL'][life.world()['transport']]} transport)"),
-                       "partition": partition + (" + loopback (the shard its own neighbour)" if a.loopback else ""), "temporal_kernel": a.temporal if temporal else "one-generation",
+                       "partition": partition + (" + loopback (the shard its own neighbour)" if a.loopback else ""), "kernel_path": path,
                        "generations_per_exchange": lay.generations_per_exchange, "live_cells_end": live},
             "roofline": roofline,
         }

@@ -220,13 +220,8 @@ int life_dev_set_timing(life_dev *d, int on);
  * identical either way (tests switch them to reach every kernel). */
 #define LIFE_OPT_SMALL_GRID 1
 #define LIFE_OPT_OVERLAP 2
-/* LIFE_OPT_SWEEP (default 0): 1 runs temporal layouts on the sweep stencil --
- * one wave per column strip x row segment with the launch's m generations
- * pipelined down the segment (life_sweep.hip); 0: the tiled
- * stencil (8-wave workgroups holding a window of rows for all m
- * generations, life_kernels.hip tstep_kernel), measured faster.  Same
- * results either way. */
-#define LIFE_OPT_SWEEP 3
+/* (option 3, the sweep stencil, was removed: slower than the tiles in every
+ * measured case, profiles/r02/sweep_ab.txt) */
 /* LIFE_OPT_BLOCK_GENS: the tiled stencil's generations per launch at most
  * (1..32, capped by generations_per_exchange; 0: the default, 20 for bits
  * and 32 for bytes, or LIFE_BLOCK_GENS from the environment).  A step call of
@@ -256,16 +251,27 @@ int life_dev_set_timing(life_dev *d, int on);
  * are identical either way.  The grid must be at least one halo deep
  * (generations_per_exchange rows). */
 #define LIFE_OPT_LOOPBACK 6
-/* LIFE_OPT_FLOW (default 0, or LIFE_FLOW from the environment): a step call
+/* LIFE_OPT_FLOW (default 1, or LIFE_FLOW from the environment): a step call
  * on a single shard whose axes both wrap inside it (bit encoding, width a
  * multiple of 32) runs its whole passes of m generations (m = the block
  * size, LIFE_OPT_BLOCK_GENS) as ONE persistent launch: workgroups pull
  * (pass, tile) items in order and a tile starts when the tiles its window
  * reads have finished the previous pass, so no pass boundary drains the chip;
  * the remainder runs as an ordinary launch.  1: write-through hand-off
- * stores; 2: plain stores + a release fence per tile.  Same results. */
+ * stores; 2: plain stores + a release fence per tile; + 4: the byte
+ * encoding too (default off, or LIFE_FLOW_BYTE=1).  Same results. */
 #define LIFE_OPT_FLOW 7
 int life_dev_configure(life_dev *d, int option, int value);
+/* The kernel family that ran the bulk of the last life_dev_step call:
+ * LIFE_PATH_ONEGEN (one generation per launch), _TILES (temporally blocked
+ * tiles, one launch per pass), _FLOW (the dataflow tiles, LIFE_OPT_FLOW),
+ * _SMALL (a small-grid resident kernel); _NONE before the first step. */
+#define LIFE_PATH_NONE 0
+#define LIFE_PATH_ONEGEN 1
+#define LIFE_PATH_TILES 2
+#define LIFE_PATH_FLOW 3
+#define LIFE_PATH_SMALL 5
+int life_dev_last_path(life_dev *d);
 int life_dev_kernel_stats(life_dev *d, double *avg_ms, int64_t *launches, double *bytes_per_launch);
 /* The same timed launches: mean cell-updates per launch (cells x generations
  * it advanced) and mean VALU lane-operations per launch (op-count model of

@@ -117,11 +117,17 @@ static const int kEnvBlockGens = [] {
     const int v = e ? atoi(e) : 0;
     return v >= 1 && v <= 32 ? v : 0;
 }();
-// LIFE_FLOW (0/1/2) sets LIFE_OPT_FLOW's default at load time.
+// LIFE_FLOW (0/1/2) sets LIFE_OPT_FLOW's default at load time; default 1:
+// 65536^2 95 -> 100 T, 32768^2 78 -> 90 T at 20 generations per pass
+// (profiles/r02/flow_ab.txt, flow_sweep.txt).
 static const int kEnvFlow = [] {
     const char *e = getenv("LIFE_FLOW");
-    const int v = e ? atoi(e) : 0;
-    return v >= 0 && v <= 2 ? v : 0;
+    const int v = e ? atoi(e) : 1;
+    return v >= 0 && v <= 2 ? v : 1;
+}();
+static const bool kEnvFlowByte = [] {
+    const char *e = getenv("LIFE_FLOW_BYTE");
+    return e ? atoi(e) != 0 : false;
 }();
 static int default_block_gens(int kernel) {
     return kEnvBlockGens ? kEnvBlockGens : (kernel == LIFE_KERNEL_BIT ? 20 : 32);
@@ -137,13 +143,13 @@ struct life_dev {
     bool timing = false;
     bool overlap = true;
     int block_gens = 0;  // tiles: generations per launch at most (LIFE_OPT_BLOCK_GENS; default_block_gens)
-    bool sweep = false;  // temporal layouts: sweep_kernel (LIFE_OPT_SWEEP 1) or tstep_kernel tiles (0, default:
-                         // faster by measurement, profiles/r02/sweep_ab.txt)
     int small_mode = 1;  // grids that fit one CU: 0 off, 1 VGPR kernel else LDS kernel, 2 LDS kernel,
                         // 3 windowed VGPR kernel over several CUs (else as 1), 4 as 1 never windowed
     int win_rows = 0, win_halo = 0;  // windowed kernel: strip height R, halo rows K (0: automatic)
     bool loop = false;  // LIFE_OPT_LOOPBACK: the one shard exchanges both axes' halos with itself
-    int flow = kEnvFlow;  // LIFE_OPT_FLOW: single-shard bit tiles as one persistent dataflow launch per
+    int last_path = LIFE_PATH_NONE;  // life_dev_last_path
+    int flow = kEnvFlow;
+    bool flow_byte = kEnvFlowByte;  // the dataflow form for the byte encoding too (LIFE_OPT_FLOW value | 4)  // LIFE_OPT_FLOW: single-shard bit tiles as one persistent dataflow launch per
                           // step call (1: write-through hand-off, 2: plain stores + release; 0 off)
     std::vector<Shard> shards;
     double acc_ms = 0.0;
@@ -532,63 +538,16 @@ int phase_end(life_dev *d, const std::vector<PhaseEvents *> &pe) {
     return LIFE_OK;
 }
 
-// Sweep launch of up to 4 (strip, segment) regions on `st` (m generations,
-// cur -> nxt), optionally timed (life::launch_sweep).
-int launch_sweeps(life_dev *d, Shard &s, const life::SweepGeom &g, const life::TileRegion *r, int nreg, int m,
-                  bool timed, hipStream_t st) {
-    const uint8_t *in = s.buf[s.cur];
-    uint8_t *out = s.buf[s.cur ^ 1];
-    TimedLaunch *t = nullptr;
-    if (d->timing && timed) {
-        int rc;
-        t = timer_slot(s, &rc);
-        if (!t) return rc;
-        HIPCHK(hipEventRecord(t->a, st));
-    }
-    HIPCHK(life::launch_sweep(s.lay, g, in, out, r, nreg, m, wrap_of(d), st));
-    if (t) {
-        HIPCHK(hipEventRecord(t->b, st));
-        const bool byte = s.lay.kernel == LIFE_KERNEL_BYTE;
-        for (int k = 0; k < nreg; k++) {
-            // owned cells of the region: strips' owned columns x segments' rows
-            // (periodic x: [lo, hi) is the whole row shifted by edge - 32 cells)
-            const int64_t xa = std::max<int64_t>(32 * (r[k].tx0 * g.sw - 1) + g.edge, g.lo);
-            const int64_t xb = std::min<int64_t>(32 * (r[k].tx1 * g.sw - g.sw - 1) + 2048 - g.edge,
-                                                 g.lo < 0 ? g.hi : std::min<int64_t>(g.hi, s.lay.w));
-            const int64_t ya = r[k].ty0 * g.seg, yb = std::min(r[k].ty1 * g.seg, s.lay.h);
-            if (xb > xa && yb > ya) {
-                const double cells = (double)(xb - xa) * (double)(yb - ya);
-                d->acc_bytes += cells * (byte ? 2.0 : 0.25);
-                d->acc_updates += cells * (double)m;
-            }
-            d->acc_valu += 64.0 * life::sweep_valu_per_lane(g, r[k], s.lay.h, m, byte);
-        }
-    }
-    return LIFE_OK;
-}
-
-// Generations the next temporal launch runs (remaining > 0): sweep launches
-// split a step call into ceil(remaining / K) nearly equal launches of an
-// instantiated stage count; tiles run min(K, remaining).
+// Generations the next temporal launch runs (remaining > 0): a step call
+// is split into ceil(remaining / bmax) launches of nearly equal size (a
+// 20-generation call runs 10 + 10, not 16 + 4); bmax = K capped by the block
+// size.
 int next_block(const life_dev *d, int64_t remaining) {
-    const life_layout &L = d->shards[0].lay;
-    const int K = L.generations_per_exchange;
-    if (!d->sweep) {
-        // tiles: ceil(remaining / bmax) launches of nearly equal size (a
-        // 20-generation call runs 10 + 10, not 16 + 4)
-        int bmax = std::min(K, 32);
-        if (d->block_gens > 0) bmax = std::min(bmax, d->block_gens);
-        const int64_t n = (remaining + bmax - 1) / bmax;
-        return (int)((remaining + n - 1) / n);
-    }
-    const int kmax = life::sweep_max_stages(L);
-    const int64_t n = (remaining + kmax - 1) / kmax;
-    const int target = (int)((remaining + n - 1) / n);
-    for (int m = target; m <= kmax && m <= remaining; ++m)
-        if (life::sweep_has(m)) return m;
-    for (int m = (int)std::min<int64_t>(remaining, kmax); m >= 1; --m)
-        if (life::sweep_has(m)) return m;
-    return 1;
+    const int K = d->shards[0].lay.generations_per_exchange;
+    int bmax = std::min(K, 32);
+    if (d->block_gens > 0) bmax = std::min(bmax, d->block_gens);
+    const int64_t n = (remaining + bmax - 1) / bmax;
+    return (int)((remaining + n - 1) / n);
 }
 
 // m <= K generations of the temporally blocked stencil on every shard, then
@@ -606,35 +565,17 @@ int generation_block(life_dev *d, int m) {
         Shard &s = d->shards[si];
         HIPCHK(hipSetDevice(s.device));
         const int64_t K = s.lay.generations_per_exchange;
-        // grid of units (tiles or strips x segments): NX x NY, unit height uh;
-        // column units [0, ca) and [cb, NX) hold the x-ring
-        int64_t NX, NY, uh, ca = 0, cb;
-        life::SweepGeom sg{};
-        if (d->sweep) {
-            sg = life::sweep_geom(s.lay, wrap_of(d).x);
-            NX = sg.nstrips;
-            NY = sg.nseg;
-            uh = sg.seg;
-            cb = NX;
-            if (rx) {
-                ca = 1;  // strip 0 owns [0, 2048 - 2 edge) >= [0, 32)
-                cb = 0;
-                while (cb < NX && 32 * (cb * sg.sw - 1) + 2048 - sg.edge <= s.lay.w - 32) ++cb;
-                cb = std::max(cb, ca);
-            }
-        } else {
-            const life::TileGeom g = life::tile_geom(s.lay, m);
-            NX = g.ntx;
-            NY = g.nty;
-            uh = g.rows;
-            cb = NX;
-            if (rx) {
-                ca = 1;
-                cb = std::max(std::min(((s.lay.w - 32) / 32) / g.words, NX), ca);
-            }
+        // grid of tiles: NX x NY, tile height uh; tile columns [0, ca) and
+        // [cb, NX) hold the x-ring
+        const life::TileGeom g = life::tile_geom(s.lay, m);
+        const int64_t NX = g.ntx, NY = g.nty, uh = g.rows;
+        int64_t ca = 0, cb = NX;
+        if (rx) {
+            ca = 1;
+            cb = std::max(std::min(((s.lay.w - 32) / 32) / g.words, NX), ca);
         }
         auto launch = [&](const life::TileRegion *r, int n, bool timed, hipStream_t st) -> int {
-            return d->sweep ? launch_sweeps(d, s, sg, r, n, m, timed, st) : launch_tiles(d, s, r, n, m, timed, st);
+            return launch_tiles(d, s, r, n, m, timed, st);
         };
         if (!(rx || ry)) {
             const life::TileRegion all{0, NX, 0, NY};
@@ -959,8 +900,8 @@ static int step_small(life_dev *d, int64_t generations) {
 // the call takes the per-launch path.
 static int step_flow(life_dev *d, int64_t generations, int64_t *done) {
     *done = 0;
-    if (!d->flow || d->sweep || d->shards.size() != 1 || d->world != 1 || d->kernel != LIFE_KERNEL_BIT ||
-        part(d, 0) || part(d, 1) || self_wrap_x(d))
+    if (!d->flow || d->shards.size() != 1 || d->world != 1 || part(d, 0) || part(d, 1) ||
+        self_wrap_x(d) || (d->kernel == LIFE_KERNEL_BYTE && !d->flow_byte))
         return LIFE_OK;
     Shard &s = d->shards[0];
     const life_layout &L = s.lay;
@@ -995,9 +936,10 @@ static int step_flow(life_dev *d, int64_t generations, int64_t *done) {
         HIPCHK(hipEventRecord(t->b, s.stream));
         t->launches = (int)passes;  // stats: mean per pass
         const double cells = (double)L.w * (double)L.h;
-        d->acc_bytes += (double)passes * cells * 0.25;
+        const bool byte = d->kernel == LIFE_KERNEL_BYTE;
+        d->acc_bytes += (double)passes * cells * (byte ? 2.0 : 0.25);
         d->acc_updates += (double)passes * cells * (double)m;
-        d->acc_valu += (double)passes * (double)(g.ntx * g.nty) * 64.0 * life::tstep_valu_per_tile_lane(m, false);
+        d->acc_valu += (double)passes * (double)(g.ntx * g.nty) * 64.0 * life::tstep_valu_per_tile_lane(m, byte);
     }
     if (passes & 1) s.cur ^= 1;
     s.flow_used = true;
@@ -1019,6 +961,7 @@ int life_dev_step(life_dev *d, int64_t generations) {
         HIPCHK(hipStreamWaitEvent(s.comm_stream, s.ev_entry, 0));
     }
     if (small_grid(d)) {
+        d->last_path = LIFE_PATH_SMALL;
         constexpr int64_t kChunk = 1 << 20;  // generations per resident launch
         for (int64_t g = 0; g < generations; g += kChunk)
             CHK(step_small(d, generations - g < kChunk ? generations - g : kChunk));
@@ -1029,6 +972,7 @@ int life_dev_step(life_dev *d, int64_t generations) {
     if (temporal(d)) {
         int64_t done = 0;
         CHK(step_flow(d, generations, &done));
+        d->last_path = done > 0 ? LIFE_PATH_FLOW : LIFE_PATH_TILES;
         for (int64_t g = done; g < generations;) {
             const int m = next_block(d, generations - g);
             CHK(generation_block(d, m));
@@ -1036,9 +980,12 @@ int life_dev_step(life_dev *d, int64_t generations) {
         }
         return LIFE_OK;
     }
+    d->last_path = LIFE_PATH_ONEGEN;
     for (int64_t g = 0; g < generations; g++) CHK(generation(d));
     return LIFE_OK;
 }
+
+int life_dev_last_path(life_dev *d) { return d ? d->last_path : LIFE_EINVAL; }
 
 int life_device_count(void) {
     int n = 0;
@@ -1278,13 +1225,10 @@ int life_dev_configure(life_dev *d, int option, int value) {
         if (value < 0 || value > 32) return LIFE_EINVAL;
         d->block_gens = value > 0 ? value : default_block_gens(d->kernel);
         return LIFE_OK;
-    case LIFE_OPT_SWEEP:
-        if (value < 0 || value > 1) return LIFE_EINVAL;
-        d->sweep = value != 0;
-        return LIFE_OK;
     case LIFE_OPT_FLOW:
-        if (value < 0 || value > 2) return LIFE_EINVAL;
-        d->flow = value;
+        if (value < 0 || (value & 3) > 2 || value > 6) return LIFE_EINVAL;
+        d->flow = value & 3;
+        d->flow_byte = (value & 4) != 0;
         return LIFE_OK;
     case LIFE_OPT_LOOPBACK: {
         if (value < 0 || value > 1) return LIFE_EINVAL;

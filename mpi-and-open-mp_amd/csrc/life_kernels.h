@@ -64,7 +64,7 @@ int tile_ghost(const life_layout &L, int m);  // ghost rows per window end: m (b
 // the last tile's window (<= 8 waves x 96 rows) may read past the bottom
 // apron without clamping.
 constexpr int64_t kTemporalSlackRows = 8 * 96;
-// Dataflow form of the bit tiles (tflow_kernel): `passes` launches of m
+// Dataflow form of the tiles (tflow_kernel): `passes` launches of m
 // generations over a single shard whose axes both wrap inside it, as ONE
 // persistent launch (no drain between passes).  `head` (2 words: the queue
 // head, then an error word the caller zeroes once and reads: 1 + an item
@@ -74,7 +74,7 @@ constexpr int64_t kTemporalSlackRows = 8 * 96;
 // Pass p reads `in` for even p and `out` for odd p: after it, the result is
 // in `out` when passes is odd, else in `in`.
 bool flow_ok(const life_layout &L, int m);
-int flow_slots();  // resident workgroups of the dataflow kernel on this device
+int flow_slots(const life_layout &L);  // resident workgroups of L's dataflow kernel on this device
 hipError_t launch_tflow(const life_layout &L, const uint8_t *in, uint8_t *out, int m, int64_t passes,
                         unsigned int *head, unsigned int *done, Wrap wrap, int flow, hipStream_t s);
 // Up to 4 disjoint tile regions in one launch.
@@ -86,25 +86,6 @@ int temporal_rows(bool bit);      // register rows per wave (32/40/48/56/64/96)
 // checked against the SQ_INSTS_VALU counter in profiles/); x 64 lanes x tiles.
 double tstep_valu_per_tile_lane(int m, bool byte);
 void set_temporal_rows(int kernel, int nr);  // kernel -1: both encodings
-
-// Sweep stencil (sweep_kernel, the default temporal kernel): one wave per
-// column strip x row segment, m generations pipelined down the segment.
-// Strip s covers window words [s*sw - 1, s*sw + 63) and owns the window cells
-// [edge, 2048 - edge) of them inside [lo, hi); segments are `seg` owned rows.
-// Regions are TileRegions in (strip, segment) units.
-struct SweepGeom {
-    int edge;                // ghost cells per strip side: 16 (K <= 16) or 32
-    int64_t sw;              // strip stride in words (63 / 62)
-    int64_t lo, hi;          // owned cells of a row (whole words; periodic x: lo = edge - 32)
-    int64_t nstrips, seg, nseg;
-};
-SweepGeom sweep_geom(const life_layout &L, bool wrapx);
-int sweep_max_stages(const life_layout &L);  // generations one launch may run
-bool sweep_has(int m);                       // a kernel instance with m stages exists
-hipError_t launch_sweep(const life_layout &L, const SweepGeom &g, const uint8_t *in, uint8_t *out,
-                        const TileRegion *r, int nreg, int m, Wrap wrap, hipStream_t s);
-// VALU instructions one lane position of the region's waves issues (model).
-double sweep_valu_per_lane(const SweepGeom &g, const TileRegion &r, int64_t h, int m, bool byte);
 
 // LDS-resident path for small single-shard grids: all `gens` generations in
 // one single-workgroup launch (in -> out; in may equal out).  Usable when

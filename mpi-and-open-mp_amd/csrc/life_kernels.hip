@@ -243,13 +243,15 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs a) {
 // ------------------------------------------------------------------ temporal
 // Temporally blocked stencils (layouts with generations_per_exchange = K
 // > 1): m <= K generations per launch, each cell read once from and written
-// once to HBM per launch (plus the ghost rows of its window).  Two kernels:
+// once to HBM per pass (plus the ghost rows of its window).  One tile body
+// (tile_body: an 8-wave workgroup per 62-word x (8R - 2m)-row tile, all m
+// generations of the tile in registers with one barrier per generation) in
+// two launch forms:
 //
-//  * sweep_kernel (default): one WAVE per column strip x row segment, the
-//    m generations pipelined down the segment (see below);
-//  * tstep_kernel: one 8-wave workgroup per 62-word x (8R - 2m)-row tile,
-//    all m generations of the tile in registers with one barrier per
-//    generation (LIFE_OPT_SWEEP 0).
+//  * tstep_kernel: one launch per pass, up to 4 tile regions (the boundary
+//    ring of a partitioned shard, or the whole shard);
+//  * tflow_kernel: every pass of a step call on a single wrapped shard in
+//    one persistent launch, tiles handed from pass to pass (LIFE_OPT_FLOW).
 
 constexpr int kStackWaves = 8;  // tstep: waves per workgroup (2 per SIMD)
 struct TArgs {
@@ -294,17 +296,34 @@ __device__ __forceinline__ void bit_hsum(uint32_t v, uint32_t &s0, uint32_t &s1)
 // Bit: centred frame (bit_hsum); byte: drifting frame (bit_hsum_drift; +2 %
 // there, -1 % for bit: profiles/r01/drift_ab.jsonl).
 //
-// FLOW (tflow_kernel, bit only): the window is loaded with agent-scope
-// (`sc1`, L1-bypassing) loads, and stored with `sc1` write-through stores
-// (FLOW 1) or plain stores (FLOW 2, the kernel releases them with a fence):
-// the rows are another workgroup's output of the same launch.
+// FLOW (tflow_kernel): the window is loaded with agent-scope (`sc1`,
+// L1-bypassing) loads, and stored with `sc1` write-through stores (FLOW 1)
+// or plain stores (FLOW 2, the kernel releases them with a fence): the rows
+// are another workgroup's output of the same launch.  Bit: 4-B atomic-form
+// loads / stores; byte: 16-B buffer loads / stores with the sc1 bit, one
+// buffer resource per row (a 65536^2 byte shard exceeds a resource's 32-bit
+// range).
 using Xch = uint32_t[2][kStackWaves][4][64];  // [parity][wave][top s0/s1, bottom s0/s1][lane]
+
+constexpr int kSc1 = 16;                  // buffer cache policy: sc1 (gfx94x/gfx950 CPol::SC1)
+constexpr int kRsrcFlags = 0x00020000;    // buffer resource dword 3 (gfx9 raw buffer, 32-bit data format)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const uint8_t *row, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(row), 0, (int)bytes, kRsrcFlags);
+}
+__device__ __forceinline__ uint4 load16_sc1(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+    const auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, kSc1);
+    return make_uint4(t[0], t[1], t[2], t[3]);
+}
+__device__ __forceinline__ void store16_sc1(__amdgpu_buffer_rsrc_t rs, uint32_t off, uint4 v) {
+    using V4 = unsigned int __attribute__((ext_vector_type(4)));
+    const V4 t = {v.x, v.y, v.z, v.w};
+    __builtin_amdgcn_raw_buffer_store_b128(t, rs, (int)off, 0, kSc1);
+}
 
 template <bool BYTE, int R, int GK, bool WRAPX, bool WRAPY, int FLOW>
 __device__ __forceinline__ void tile_body(const TArgs &a, const uint8_t *in, uint8_t *out, int64_t tx, int64_t ty,
                                           Xch &xch) {
     static_assert(R >= 3 && GK >= 0 && GK <= 32, "window");
-    static_assert(FLOW == 0 || !BYTE, "dataflow tiles: bit encoding");
     constexpr int NW = kStackWaves;
     // the window's ghost rows at each end: GK, or (GK = 0) the launch's
     // generations m <= 32 (checked on the host); after m generations rows
@@ -342,7 +361,10 @@ __device__ __forceinline__ void tile_body(const TArgs &a, const uint8_t *in, uin
     uint32_t v[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        if (BYTE) {
+        if (BYTE && FLOW) {
+            const __amdgpu_buffer_rsrc_t rs = row_rsrc(p, a.pitch);
+            v[r] = pack32(load16_sc1(rs, voff), load16_sc1(rs, voff + 16));
+        } else if (BYTE) {
             const uint4 *q = reinterpret_cast<const uint4 *>(p + voff);
             v[r] = pack32(q[0], q[1]);
         } else if (FLOW) {
@@ -421,7 +443,11 @@ __device__ __forceinline__ void tile_body(const TArgs &a, const uint8_t *in, uin
         if (r < r0 || r >= r1) continue;
         if (DRIFT) v[r] = drift_realign(v[r], a.m);  // every lane: the bpermute reads lane + 1
         if (st && y0 + r < a.h) {
-            if (BYTE) {
+            if (BYTE && FLOW == 1) {
+                const __amdgpu_buffer_rsrc_t rs = row_rsrc(q - voff, a.pitch);  // the row: uniform
+                store16_sc1(rs, voff, unpack_half(v[r], 0));
+                store16_sc1(rs, voff + 16, unpack_half(v[r], 1));
+            } else if (BYTE) {
                 uint4 *o = reinterpret_cast<uint4 *>(q);
                 o[0] = unpack_half(v[r], 0);
                 o[1] = unpack_half(v[r], 1);
@@ -473,8 +499,9 @@ struct FArgs {
     unsigned int *done;              // per tile: passes completed (zeroed before the launch)
 };
 
-template <int R, bool WRAPX, bool WRAPY, int FLOW>
-__global__ __launch_bounds__(64 * kStackWaves, 6) void tflow_kernel(FArgs f) {  // 3 tiles per CU
+// bit: 3 tiles per CU (80 VGPRs); byte: 2 (its 92 VGPRs)
+template <bool BYTE, int R, int GK, bool WRAPX, bool WRAPY, int FLOW>
+__global__ __launch_bounds__(64 * kStackWaves, BYTE ? 4 : 6) void tflow_kernel(FArgs f) {
     __shared__ Xch xch;
     __shared__ unsigned int item_sh;
     const TArgs &a = f.t;
@@ -539,7 +566,7 @@ __global__ __launch_bounds__(64 * kStackWaves, 6) void tflow_kernel(FArgs f) {  
         __syncthreads();
         const uint8_t *in = (p & 1) ? a.out : a.in;
         uint8_t *out = const_cast<uint8_t *>((p & 1) ? a.in : a.out);
-        tile_body<false, R, 0, WRAPX, WRAPY, FLOW>(a, in, out, tx, ty, xch);
+        tile_body<BYTE, R, GK, WRAPX, WRAPY, FLOW>(a, in, out, tx, ty, xch);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
         __syncthreads();
         prev_flag = f.done + ty * f.ntx + tx;
@@ -1223,12 +1250,7 @@ hipError_t launch_k(const TArgs &a, Wrap wrap, unsigned grid, hipStream_t s) {
 
 int tile_ghost(const life_layout &L, int m) { return is_bit(L) ? m : L.generations_per_exchange; }
 
-bool flow_ok(const life_layout &L, int m) {
-    // the dependency rule reads tile rows ty-2..ty+2: a window may reach at
-    // most one tile row beyond its neighbours (m <= T)
-    const TileGeom g = tile_geom(L, m);
-    return is_bit(L) && g.rows >= m && m >= 1;
-}
+
 
 TileGeom tile_geom(const life_layout &L, int m) {
     TileGeom g;
@@ -1275,36 +1297,51 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
 }
 
 namespace {
-template <int R>
-hipError_t launch_fr(const FArgs &f, int flow, unsigned grid, hipStream_t s) {
-    constexpr unsigned kThreads = 64 * kStackWaves;
-    if (flow == 2)
-        tflow_kernel<R, true, true, 2><<<grid, kThreads, 0, s>>>(f);
-    else
-        tflow_kernel<R, true, true, 1><<<grid, kThreads, 0, s>>>(f);
-    return hipGetLastError();
+// Instances of the dataflow tiles: bit R = 40 / 48 (runtime ghost rows =
+// m), byte R = 48 with K = 16 / 32 ghost rows (compile-time, as tstep).
+template <bool BYTE, int R, int GK, int FLOW>
+const void *flow_fn() {
+    return (const void *)tflow_kernel<BYTE, R, GK, true, true, FLOW>;
+}
+const void *flow_kernel_of(const life_layout &L, int flow) {
+    const bool f2 = flow == 2;
+    if (is_bit(L)) {
+        if (temporal_rows(true) == 40) return f2 ? flow_fn<false, 40, 0, 2>() : flow_fn<false, 40, 0, 1>();
+        if (temporal_rows(true) == 48) return f2 ? flow_fn<false, 48, 0, 2>() : flow_fn<false, 48, 0, 1>();
+        return nullptr;
+    }
+    if (temporal_rows(false) != 48) return nullptr;
+    if (L.generations_per_exchange == 16) return f2 ? flow_fn<true, 48, 16, 2>() : flow_fn<true, 48, 16, 1>();
+    if (L.generations_per_exchange == 32) return f2 ? flow_fn<true, 48, 32, 2>() : flow_fn<true, 48, 32, 1>();
+    return nullptr;
 }
 }  // namespace
 
-int flow_slots() {
-    static const int slots = [] {
-        int dev = 0, cus = 0, per = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            return 0;
-        const void *fn = temporal_rows(true) == 40 ? (const void *)tflow_kernel<40, true, true, 1>
-                                                   : (const void *)tflow_kernel<48, true, true, 1>;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 64 * kStackWaves, 0) != hipSuccess) return 0;
-        return cus * per;
-    }();
-    return slots;
+bool flow_ok(const life_layout &L, int m) {
+    // an instance for this encoding / tile height / apron depth, and the
+    // dependency rule reads tile rows ty-2..ty+2: a window may reach at most
+    // one tile row beyond its neighbours (ghost rows <= T); byte tiles hold
+    // K ghost rows whatever m
+    if (!flow_kernel_of(L, 1) || m < 1) return false;
+    const TileGeom g = tile_geom(L, m);
+    return g.rows >= tile_ghost(L, m);
+}
+
+int flow_slots(const life_layout &L) {
+    const void *fn = flow_kernel_of(L, 1);
+    int dev = 0, cus = 0, per = 0;
+    if (!fn || hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 64 * kStackWaves, 0) != hipSuccess)
+        return 0;
+    return cus * per;
 }
 
 hipError_t launch_tflow(const life_layout &L, const uint8_t *in, uint8_t *out, int m, int64_t passes,
                         unsigned int *head, unsigned int *done, Wrap wrap, int flow, hipStream_t s) {
-    const int R = temporal_rows(true);
-    if (!is_bit(L) || !wrap.x || !wrap.y || m < 1 || m > 32 ||
-        m > L.generations_per_exchange || passes < 1 || (R != 40 && R != 48) || !flow_ok(L, m))
+    const void *fn = flow_kernel_of(L, flow);
+    if (!fn || !wrap.x || !wrap.y || m < 1 || m > 32 || m > L.generations_per_exchange || passes < 1 ||
+        !flow_ok(L, m))
         return hipErrorInvalidValue;
     const TileGeom g = tile_geom(L, m);
     FArgs f{};
@@ -1325,10 +1362,13 @@ hipError_t launch_tflow(const life_layout &L, const uint8_t *in, uint8_t *out, i
     hipError_t e = hipMemsetAsync(head, 0, sizeof(unsigned int), s);  // the error word is the caller's
     if (e == hipSuccess) e = hipMemsetAsync(done, 0, sizeof(unsigned int) * (size_t)(g.ntx * g.nty), s);
     if (e != hipSuccess) return e;
-    const int slots = flow_slots();
-    if (slots <= 0) return hipErrorInvalidValue;
-    const unsigned grid = (unsigned)std::min<int64_t>(f.items, slots);
-    return R == 40 ? launch_fr<40>(f, flow, grid, s) : launch_fr<48>(f, flow, grid, s);
+    static int slots[2] = {0, 0};  // per encoding: resident workgroups (occupancy query, once)
+    int &n = slots[is_bit(L) ? 1 : 0];
+    if (n <= 0) n = flow_slots(L);
+    if (n <= 0) return hipErrorInvalidValue;
+    const unsigned grid = (unsigned)std::min<int64_t>(f.items, n);
+    void *args[] = {&f};
+    return hipLaunchKernel(fn, dim3(grid), dim3(64 * kStackWaves), args, 0, s);
 }
 
 int reg_small_rows(const life_layout &L) {

@@ -41,7 +41,7 @@ KERNELS = {"byte": KERNEL_BYTE, "bit": KERNEL_BIT}
 XPORT_AUTO, XPORT_RCCL, XPORT_LOCAL = 0, 1, 2
 HALO_SEND, HALO_RECV, HALO_FILL = 0, 1, 2
 HALO_COLUMN, HALO_ROW = 0, 1
-OPT_SMALL_GRID, OPT_OVERLAP, OPT_SWEEP, OPT_SMALL_WINDOW, OPT_BLOCK_GENS, OPT_LOOPBACK, OPT_FLOW = 1, 2, 3, 4, 5, 6, 7
+OPT_SMALL_GRID, OPT_OVERLAP, OPT_SMALL_WINDOW, OPT_BLOCK_GENS, OPT_LOOPBACK, OPT_FLOW = 1, 2, 4, 5, 6, 7
 # LIFE_TEMPORAL_DEPTH(_BYTE): generations per halo exchange of the temporal layouts
 TEMPORAL_DEPTH = {"bit": 32, "byte": 32}
 BLOCK_GENS = {"bit": 20, "byte": 32}  # tiles: default generations per launch at most (LIFE_OPT_BLOCK_GENS)
@@ -56,8 +56,9 @@ ABI_SYMBOLS = (
     "life_dev_layout", "life_dev_world", "life_dev_set_timing", "life_dev_kernel_stats",
     "life_tune", "life_tune_temporal", "life_dev_configure", "life_dev_kernel_work", "life_dev_checksum",
     "life_dev_gather_vtk", "life_dev_destroy", "life_measure_copy", "life_dev_phase_stats",
-    "life_dev_barrier", "life_device_count",
+    "life_dev_barrier", "life_device_count", "life_dev_last_path",
 )
+PATHS = {0: "none", 1: "onegen", 2: "tiles", 3: "flow", 5: "small"}
 
 
 class LifeError(RuntimeError):
@@ -140,6 +141,7 @@ def _lib():
         L.life_dev_sync.argtypes = [vp]
         L.life_dev_barrier.argtypes = [vp]
         L.life_device_count.argtypes = []
+        L.life_dev_last_path.argtypes = [vp]
         L.life_dev_checksum.argtypes = [vp, P(ctypes.c_uint64)]
         L.life_dev_layout.argtypes = [vp, i32, P(Layout)]
         L.life_dev_world.argtypes = [vp] + [P(ctypes.c_int)] * 5
@@ -250,7 +252,7 @@ class Life:
     """
 
     def __init__(self, nx: int, ny: int, shards: int = 1, kernel="bit", dims=(0, 0),
-                 transport: int = XPORT_AUTO, small_grid: bool = True, overlap: bool = True, sweep=None,
+                 transport: int = XPORT_AUTO, small_grid: bool = True, overlap: bool = True, flow=None,
                  window=None, _handle=None):
         self.nx, self.ny = int(nx), int(ny)
         self.kernel = kernel_id(kernel)
@@ -273,10 +275,10 @@ class Life:
             self.configure(OPT_SMALL_WINDOW, int(window[0]) * 256 + int(window[1]))
         if not overlap:
             self.configure(OPT_OVERLAP, 0)
-        # sweep: None (library default: the tiled temporal stencil), True (the
-        # sweep stencil), or False
-        if sweep is not None:
-            self.configure(OPT_SWEEP, int(bool(sweep)))
+        # flow: None (library default: the dataflow tiles where they apply),
+        # or a LIFE_OPT_FLOW value (0: one launch per pass)
+        if flow is not None:
+            self.configure(OPT_FLOW, int(flow))
 
     def configure(self, option: int, value: int) -> None:
         _check(_lib().life_dev_configure(self._h, option, value), "configure")
@@ -342,6 +344,13 @@ class Life:
 
     def set_timing(self, on: bool) -> None:
         _check(_lib().life_dev_set_timing(self._h, int(on)), "set_timing")
+
+    def last_path(self) -> str:
+        """Kernel family of the last step call (life_dev_last_path)."""
+        return PATHS[_check(_lib().life_dev_last_path(self._h), "last_path")]
+
+    def flow_active(self) -> bool:
+        return self.last_path() == "flow"
 
     def kernel_stats(self):
         ms, n, b = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()

@@ -33,7 +33,11 @@ VARIANTS = {  # variant -> (kernel-name substring, calibrated 16-B access)
     "byte_onegen": ("step_kernel<life::(anonymous namespace)::ByteEnc", True),
     "bit_temporal": ("tstep_kernel<false", True),    # 4 B per lane (calib_4b)
     "byte_temporal": ("tstep_kernel<true", True),    # 2 x 16 B per lane
+    "bit_flow": ("tflow_kernel<", True),             # 4 B per lane, sc1; one dispatch = PASSES[var] passes
 }
+# dataflow launches run several passes per dispatch: the PMC job times a
+# 80-generation call at 20 generations per pass (profiles/r02/jobs/r2r.sh)
+PASSES = {"bit_flow": 4}
 
 out = {}
 for var, (needle, calibrated) in VARIANTS.items():
@@ -48,7 +52,7 @@ for var, (needle, calibrated) in VARIANTS.items():
         # the longest dispatches are the full-length launches
         durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
         full = [float(r["Counter_Value"]) for r, t in zip(rows, durs) if t >= 0.8 * max(durs)]
-        vals[c] = statistics.median(full) * 1024.0
+        vals[c] = statistics.median(full) * 1024.0 / PASSES.get(var, 1)
     if len(vals) != 2:
         continue
     key = f"{var}_{size}"

@@ -29,6 +29,7 @@ def test_flow_parity(gpu, oracle, nx, ny, gens, m, flow):
         life.upload(g0)
         life.set_timing(True)
         life.step(gens)
+        assert life.last_path() == "flow"
         avg_ms, launches, _ = life.kernel_stats()
         assert launches >= gens // m  # the passes were timed as one launch each
         np.testing.assert_array_equal(life.gather(), want)
@@ -42,15 +43,18 @@ def test_flow_fullsize_census(gpu, n, m, flow):
     count) equals the per-launch tiles' after the same generations."""
     gens = 7 * m + 3
     with gpu.Life(n, n, kernel="bit") as ref:
+        ref.configure(gpu.OPT_FLOW, 0)  # the per-launch tiles
         ref.configure(gpu.OPT_BLOCK_GENS, m)
         ref.fill_random(5, 0.5)
         ref.step(gens)
+        assert ref.last_path() == "tiles"
         want = (ref.checksum(), ref.live_count())
     with gpu.Life(n, n, kernel="bit") as life:
         life.configure(gpu.OPT_FLOW, flow)
         life.configure(gpu.OPT_BLOCK_GENS, m)
         life.fill_random(5, 0.5)
         life.step(gens)
+        assert life.last_path() == "flow"
         assert (life.checksum(), life.live_count()) == want
 
 
@@ -58,3 +62,33 @@ def test_flow_rejected_options(gpu):
     with gpu.Life(256, 256, kernel="bit") as life:
         with pytest.raises(RuntimeError):
             life.configure(gpu.OPT_FLOW, 3)
+
+
+# byte encoding (LIFE_OPT_FLOW value | 4: opt-in): 16-B sc1 buffer loads /
+# stores, K ghost rows per window whatever the pass size
+@pytest.mark.parametrize("nx,ny,gens", [(2048, 1000, 70), (1024, 3000, 64), (96, 700, 33)])
+def test_flow_byte_parity(gpu, oracle, nx, ny, gens):
+    g0 = oracle.fill_random(nx, ny, seed=23, density=0.45)
+    want = oracle.life_run(g0, gens)
+    with gpu.Life(nx, ny, kernel="byte", small_grid=False) as life:
+        life.configure(gpu.OPT_FLOW, 1 | 4)
+        life.configure(gpu.OPT_BLOCK_GENS, 16)
+        life.upload(g0)
+        life.step(gens)
+        assert life.last_path() == "flow"
+        np.testing.assert_array_equal(life.gather(), want)
+
+
+def test_flow_byte_fullsize_census(gpu):
+    n, gens = 32768, 3 * 32 + 7
+    with gpu.Life(n, n, kernel="byte") as ref:
+        ref.configure(gpu.OPT_FLOW, 0)
+        ref.fill_random(8, 0.5)
+        ref.step(gens)
+        want = (ref.checksum(), ref.live_count())
+    with gpu.Life(n, n, kernel="byte") as life:
+        life.configure(gpu.OPT_FLOW, 1 | 4)
+        life.fill_random(8, 0.5)
+        life.step(gens)
+        assert life.last_path() == "flow"
+        assert (life.checksum(), life.live_count()) == want

@@ -76,36 +76,39 @@ def test_byte_equals_bit_long(gpu, oracle, nx):
     np.testing.assert_array_equal(out["bit"], oracle.life_run(g0, gens, threads=4))
 
 
-@pytest.mark.parametrize("sweep", [True, False], ids=["sweep", "tiles"])
+@pytest.mark.parametrize("flow", [0, 1], ids=["tiles", "flow"])
 @pytest.mark.parametrize("kernel,nx,gens", [("bit", 4096, 40), ("bit", 31, 13), ("byte", 4096, 40), ("byte", 31, 13)])
-def test_timing_stats(gpu, kernel, nx, gens, sweep):
+def test_timing_stats(gpu, kernel, nx, gens, flow):
     """One timed launch per generation (one-generation kernels: a block
     narrower than the 32-cell apron) or per up to K generations (temporal
     kernels).  Bytes are the compulsory HBM traffic: 0.25 B (bit) / 2 B
     (byte) per cell per LAUNCH; cell-updates are cells x generations; VALU
-    lane-ops are modelled for the temporal kernels only."""
+    lane-ops are modelled for the temporal kernels only.  The dataflow tiles
+    (flow, bit) count each of their passes as one launch."""
     K = gpu.TEMPORAL_DEPTH[kernel]
     temporal = nx >= 32
-    # ceil(gens / bmax) launches of nearly equal size; bmax: sweep = K capped
-    # by the largest sweep instance (16), tiles = K capped by BLOCK_GENS
-    bmax = min(K, 16) if sweep else min(K, 32, gpu.BLOCK_GENS[kernel])
+    # ceil(gens / bmax) launches of nearly equal size, bmax = K capped by
+    # BLOCK_GENS (the dataflow passes: gens // bmax of bmax, here exact)
+    bmax = min(K, 32, gpu.BLOCK_GENS[kernel])
     sizes, left = [], gens
     while temporal and left:
         n = -(-left // bmax)
         sizes.append(-(-left // n))
         left -= sizes[-1]
     launches = len(sizes) if temporal else gens
-    with gpu.Life(nx, 4096, kernel=kernel, small_grid=False, sweep=sweep) as life:
+    with gpu.Life(nx, 4096, kernel=kernel, small_grid=False, flow=flow) as life:
         life.fill_random(1)
         life.set_timing(True)
         life.step(gens)
+        assert life.last_path() == ("flow" if flow and kernel == "bit" and temporal else
+                                    "tiles" if temporal else "onegen")
         ms, n, b = life.kernel_stats()
         upd, valu = life.kernel_work()
         assert n == launches and ms > 0
         assert n * b == pytest.approx(nx * 4096 * launches * (0.25 if kernel == "bit" else 2.0))
         assert n * upd == pytest.approx(nx * 4096 * gens)
         assert (valu > 0) == temporal
-        if temporal and not sweep:  # 3 x ceil(4096 / (8 waves x R rows - 2m)) tiles of 62 words, 64 lanes;
+        if temporal:  # 3 x ceil(4096 / (8 waves x R rows - 2m)) tiles of 62 words, 64 lanes;
             # byte: + pack/unpack (35 ops per register row per launch)
             R = gpu.TEMPORAL_ROWS[kernel]
             want = 0
@@ -116,13 +119,6 @@ def test_timing_stats(gpu, kernel, nx, gens, sweep):
                 per_row = (12 if kernel == "byte" else 13) * m + (35 if kernel == "byte" else 0)
                 want += tiles * 64 * 8 * R * per_row
             assert n * valu == pytest.approx(want)
-        if temporal and sweep:
-            # 12 VALU per 64-lane x 32-cell stage-step = 0.375 lane-ops per
-            # cell-update, plus ghost work (x: 2 of 64 lanes + overhang; y:
-            # the stage ramp) and, for bytes, pack/unpack
-            per_update = valu / upd
-            # (4096 wide: 3 strips of 64 lanes for 128 words)
-            assert 0.375 < per_update < (1.0 if kernel == "bit" else 1.6), per_update
 
 
 # ---------------------------------------------------------------- temporal blocking (bit)
@@ -132,18 +128,19 @@ def test_timing_stats(gpu, kernel, nx, gens, sweep):
                                    # widths not a multiple of 32: the shard wraps its own x-aprons
                                    (33, 9), (63, 64), (500, 500), (1000, 37), (4016, 130), (1985, 3), (2047, 200),
                                    (256, 5000), (100, 3001)])
-@pytest.mark.parametrize("sweep", [True, False], ids=["sweep", "tiles"])
-def test_temporal_single_shard(gpu, oracle, kernel, nx, ny, sweep):
+@pytest.mark.parametrize("flow", [0, 5], ids=["tiles", "flow"])
+def test_temporal_single_shard(gpu, oracle, kernel, nx, ny, flow):
     """Blocks at least 32 cells wide take the temporally blocked kernel (up to
-    K generations per launch); runs of 1, 7, 8, 9, 20 and 40 generations.
-    sweep: the sweep stencil (one wave per strip x segment); tiles: the
-    8-wave tiled stencil."""
+    K generations per launch); runs of 1, 7, 8, 9, 20, 40 and 70 generations.
+    tiles: one launch per pass; flow: LIFE_OPT_FLOW 1 | 4, the dataflow tiles
+    for both encodings where the shard wraps x in its words (the 40- and
+    70-generation calls)."""
     assert gpu.layout_query(nx, ny, (1, 1), 0, kernel).generations_per_exchange == gpu.TEMPORAL_DEPTH[kernel]
     g0 = oracle.fill_random(nx, ny, seed=nx + 3 * ny, density=0.5)
-    with gpu.Life(nx, ny, kernel=kernel, small_grid=False, sweep=sweep) as life:
+    with gpu.Life(nx, ny, kernel=kernel, small_grid=False, flow=flow) as life:
         life.upload(g0)
         done = 0
-        for n in (1, 7, 8, 9, 20, 40):
+        for n in (1, 7, 8, 9, 20, 40, 70):
             life.step(n)
             done += n
             np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, done, threads=4),
@@ -157,8 +154,7 @@ def test_temporal_single_shard(gpu, oracle, kernel, nx, ny, sweep):
     (500, 500, 2, (2, 1)), (500, 300, 8, (4, 2)), (100, 64, 6, (3, 2)), (1000, 70, 4, (2, 2)), (2047, 90, 2, (1, 2)),
 ])
 @pytest.mark.parametrize("kernel", ["bit", "byte"])
-@pytest.mark.parametrize("sweep", [True, False], ids=["sweep", "tiles"])
-def test_temporal_multi_shard_local(gpu, oracle, kernel, nx, ny, shards, dims, sweep):
+def test_temporal_multi_shard_local(gpu, oracle, kernel, nx, ny, shards, dims):
     """K-deep aprons through the LOCAL transport: whole-word columns, K-row
     blocks of rows, ring tiles first, interior overlapped with the exchange."""
     for r in range(shards):
@@ -166,7 +162,7 @@ def test_temporal_multi_shard_local(gpu, oracle, kernel, nx, ny, shards, dims, s
         want = K if dims[1] == 1 or ny // dims[1] >= K else 1
         assert gpu.layout_query(nx, ny, dims, r, kernel).generations_per_exchange == want
     g0 = oracle.fill_random(nx, ny, seed=7 * shards + ny, density=0.45)
-    with gpu.Life(nx, ny, shards=shards, kernel=kernel, dims=dims, transport=gpu.XPORT_LOCAL, sweep=sweep) as life:
+    with gpu.Life(nx, ny, shards=shards, kernel=kernel, dims=dims, transport=gpu.XPORT_LOCAL) as life:
         life.upload(g0)
         done = 0
         for n in (1, 8, 13, 16, 30, 40):
@@ -183,7 +179,7 @@ def test_temporal_tile_heights_agree(gpu, oracle, kernel, rows):
     g0 = oracle.fill_random(nx, ny, seed=rows, density=0.5)
     gpu.tune_temporal(rows, kernel)
     try:
-        with gpu.Life(nx, ny, kernel=kernel, small_grid=False, sweep=False) as life:
+        with gpu.Life(nx, ny, kernel=kernel, small_grid=False) as life:
             life.upload(g0)
             life.step(40)
             np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, 40, threads=4))
