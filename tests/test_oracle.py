@@ -108,3 +108,22 @@ def test_checksum_definition(oracle):
     parts = sum(oracle.checksum(big[y0:y0 + 100, x0:x0 + 150], x0, y0, 300)
                 for y0 in (0, 100) for x0 in (0, 150)) % 2**64
     assert parts == oracle.checksum(big)
+
+
+def test_ref_mpirun_cfg_and_rate(oracle, lm, tmp_path):
+    """oracle/ref_mpirun.py (bench.py's cpu_baseline "reference" leg): the .cfg
+    it writes loads back to the same grid (the reference's format,
+    life_cart.c:92-109), and the reference life_cart under mpiexec -n 4 yields
+    a positive steady-state rate."""
+    import ref_mpirun
+
+    g = oracle.fill_random(96, 64, 7, 0.5)
+    path = str(tmp_path / "r.cfg")
+    ref_mpirun.write_cfg(path, 96, 64, ref_mpirun.cfg_body(g), 11, 12)
+    steps, save, back = lm.load_cfg(path)
+    assert (steps, save) == (11, 12)
+    assert np.array_equal(back, g)
+    if not ref_mpirun.available():
+        pytest.skip("oracle/_ref/life_cart or mpiexec not built here")
+    r = ref_mpirun.steady_rate(oracle.fill_random(256, 256, 3, 0.5), 4, target_s=0.5, probe_gens=10)
+    assert r["kind"] == "reference" and r["cores"] == 4 and r["value"] > 0
