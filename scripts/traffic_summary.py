@@ -70,6 +70,14 @@ for var, (needle, calibrated) in VARIANTS.items():
                                 "source": f"profiles/{rnd}/pmc_*_{var}.csv", "calibrated": False,
                                 "note": "4 B/lane loads and stores: access width uncalibrated on gfx950 "
                                         "(MI355X_MICROARCH.md, HBM); raw counter values, not HBM bytes"}
-with open(os.path.join(ROOT, "profiles", "traffic.json"), "w") as f:
-    json.dump(out, f, indent=1)
+# merge: entries of other rounds / variants stay
+path = os.path.join(ROOT, "profiles", "traffic.json")
+try:
+    with open(path) as f:
+        merged = json.load(f)
+except (OSError, ValueError):
+    merged = {}
+merged.update(out)
+with open(path, "w") as f:
+    json.dump(merged, f, indent=1)
 print(json.dumps(out, indent=1))
