@@ -232,11 +232,15 @@ def main():
 
     def barrier_sync():
         # life.sync() = hipStreamSynchronize on every stream the library
-        # launches on (the only GPU work in this process); the barrier and
-        # max-over-ranks go through torch.distributed when N > 1.
-        life.sync()
-        if dist is not None:
-            dist.barrier()
+        # launches on (the only GPU work in this process).  Rank mode: the
+        # barrier is life_dev_barrier (an 8-byte RCCL all-reduce every rank
+        # joins, then a stream sync: tens of us) rather than a gloo TCP
+        # barrier, whose ~0.1-0.2 ms would sit inside a 20-generation timed
+        # region; max-over-ranks goes through torch.distributed.
+        if rank_mode:
+            life.barrier()
+        else:
+            life.sync()
 
     life.set_timing(True)
     barrier_sync()

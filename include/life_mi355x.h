@@ -185,6 +185,12 @@ int life_dev_gather(life_dev *d, uint8_t *grid);
  * mode).  The caller writes the 10 header lines in front (driver/life.c). */
 int life_dev_gather_vtk(life_dev *d, char *body);
 
+/* The same collect as packed rows: ny rows of ceil(nx/8) bytes, cell x at
+ * bit (x & 7) of byte (x >> 3) -- the body of the driver's LIFEBITS
+ * checkpoint frame (driver/life.c save_bits), 1/16 of the VTK text and 1/8
+ * of the dense grid over PCIe (root only in rank mode).  Blocking. */
+int life_dev_gather_bits(life_dev *d, uint8_t *packed);
+
 /* Live cells over the whole grid (all ranks). Blocking. */
 int64_t life_dev_live_count(life_dev *d);
 

@@ -1051,30 +1051,70 @@ int stage_buffer(Shard &s, size_t bytes, uint8_t **out) {
     return LIFE_OK;
 }
 
-// life_collect for `bpc` output bytes per cell: 1 = dense 0/1 cells
-// (export kernel), 2 = the VTK "%d\n" cell text (vtk kernel).  Every shard
-// exports its block on the device; in-process shards copy straight into
+// life_collect in one of three frame formats: DENSE 0/1 cells (export
+// kernel, 1 B per cell), VTK "%d\n" cell text (vtk kernel, 2 B per cell) or
+// BITS packed rows (bits kernel, LIFEBITS: bit x & 7 of byte x >> 3).  Every
+// shard exports its block on the device; in-process shards copy straight into
 // place, rank mode sends the blocks to the root (world-1) over RCCL.
-int gather_impl(life_dev *d, uint8_t *out, int bpc) {
+enum class Frame { DENSE, VTK, BITS };
+
+int gather_impl(life_dev *d, uint8_t *out, Frame fmt) {
     const int root = d->world - 1;  // life_collect: cart rank of (dims0-1, dims1-1)
     const bool have_root = find_local(d, root) != nullptr;
     if (have_root && !out) return LIFE_EINVAL;
     CHK(life_dev_sync(d));
+    const int64_t frb = fmt == Frame::BITS ? (d->nx + 7) / 8 : d->nx * (fmt == Frame::VTK ? 2 : 1);  // frame row
+    auto row_bytes = [&](const life_layout &L) -> int64_t {
+        return fmt == Frame::BITS ? life::bits_row_bytes(L) : L.w * (fmt == Frame::VTK ? 2 : 1);
+    };
     auto export_block = [&](Shard &s, uint8_t **stage) -> int {
         const life_layout &L = s.lay;
-        CHK(stage_buffer(s, (size_t)(L.w * L.h * bpc), stage));
-        if (bpc == 1)
+        CHK(stage_buffer(s, (size_t)(row_bytes(L) * L.h), stage));
+        if (fmt == Frame::DENSE)
             HIPCHK(life::launch_export_block(L, s.buf[s.cur], *stage, s.stream));
-        else
+        else if (fmt == Frame::VTK)
             HIPCHK(life::launch_vtk_block(L, s.buf[s.cur], *stage, s.stream));
+        else
+            HIPCHK(life::launch_bits_block(L, s.buf[s.cur], *stage, s.stream));
         return LIFE_OK;
     };
+    // BITS: a byte holding cells of two blocks (a block edge at x % 8 != 0)
+    // is OR-ed together from both exports; those frame bytes start at 0
+    auto shared_first = [&](const life_layout &L) { return fmt == Frame::BITS && (L.x0 & 7) != 0; };
+    auto shared_last = [&](const life_layout &L) {
+        return fmt == Frame::BITS && ((L.x0 + L.w) & 7) != 0 && L.x0 + L.w < d->nx;
+    };
+    std::vector<uint8_t> tmp;
     auto place = [&](const life_layout &L, const uint8_t *src) -> int {
-        // blocking: `out` is the caller's pageable memory
-        HIPCHK(hipMemcpy2D(out + (L.y0 * d->nx + L.x0) * bpc, (size_t)(d->nx * bpc), src, (size_t)(L.w * bpc),
-                           (size_t)(L.w * bpc), (size_t)L.h, hipMemcpyDeviceToHost));
+        const int64_t rb = row_bytes(L);
+        uint8_t *dst = out + L.y0 * frb + (fmt == Frame::BITS ? (L.x0 >> 3) : L.x0 * (fmt == Frame::VTK ? 2 : 1));
+        if (!shared_first(L) && !shared_last(L)) {
+            // blocking: `out` is the caller's pageable memory
+            HIPCHK(hipMemcpy2D(dst, (size_t)frb, src, (size_t)rb, (size_t)rb, (size_t)L.h, hipMemcpyDeviceToHost));
+            return LIFE_OK;
+        }
+        tmp.resize((size_t)(rb * L.h));
+        HIPCHK(hipMemcpy(tmp.data(), src, tmp.size(), hipMemcpyDeviceToHost));
+        const bool f = shared_first(L), l = shared_last(L);
+        for (int64_t y = 0; y < L.h; y++) {
+            uint8_t *o = dst + y * frb;
+            const uint8_t *t = tmp.data() + y * rb;
+            const int64_t a = f ? 1 : 0, b = l ? rb - 1 : rb;
+            if (b > a) memcpy(o + a, t + a, (size_t)(b - a));
+            if (f) o[0] |= t[0];
+            if (l && (rb > 1 || !f)) o[rb - 1] |= t[rb - 1];
+        }
         return LIFE_OK;
     };
+    if (fmt == Frame::BITS) {
+        // zero the shared bytes of every block boundary (all ranks' blocks)
+        for (int r = 0; r < d->world && have_root; r++) {
+            life_layout L;
+            CHK(life_layout_query(d->nx, d->ny, d->dims[0], d->dims[1], r, d->kernel, &L));
+            if (shared_first(L))
+                for (int64_t y = 0; y < L.h; y++) out[(L.y0 + y) * frb + (L.x0 >> 3)] = 0;
+        }
+    }
     if (!d->rank_mode) {
         for (Shard &s : d->shards) {
             HIPCHK(hipSetDevice(s.device));
@@ -1093,7 +1133,7 @@ int gather_impl(life_dev *d, uint8_t *out, int bpc) {
     uint8_t *stage;
     CHK(export_block(s, &stage));
     if (s.rank != root) {
-        NCCLCHK(ncclSend(stage, (size_t)(s.lay.w * s.lay.h * bpc), ncclUint8, root, s.comm, s.stream));
+        NCCLCHK(ncclSend(stage, (size_t)(row_bytes(s.lay) * s.lay.h), ncclUint8, root, s.comm, s.stream));
         HIPCHK(hipStreamSynchronize(s.stream));
         return LIFE_OK;
     }
@@ -1102,14 +1142,14 @@ int gather_impl(life_dev *d, uint8_t *out, int bpc) {
     for (int r = 0; r < d->world; r++) {
         life_layout L;
         CHK(life_layout_query(d->nx, d->ny, d->dims[0], d->dims[1], r, d->kernel, &L));
-        if (L.w * L.h > maxb) maxb = L.w * L.h;
+        if (row_bytes(L) * L.h > maxb) maxb = row_bytes(L) * L.h;
     }
     // The root's own block sits in the front of the staging buffer; two
     // receive slots follow.  Block k+1 arrives over RCCL (non-blocking
     // stream) while the host copies block k out of the other slot (a
     // blocking copy into the caller's pageable memory), so the fan-in of
     // world-1 blocks is not serialised behind the D2H copies.
-    const size_t slot = (size_t)(maxb * bpc);
+    const size_t slot = (size_t)maxb;
     {
         // grow keeping the exported block: copy it to the host first
         CHK(place(s.lay, stage));
@@ -1123,12 +1163,12 @@ int gather_impl(life_dev *d, uint8_t *out, int bpc) {
     for (size_t k = 0; k < peers.size(); k++) {
         life_layout L;
         CHK(layout_of(peers[k], &L));
-        if (k == 0) NCCLCHK(ncclRecv(stage, (size_t)(L.w * L.h * bpc), ncclUint8, peers[0], s.comm, s.stream));
+        if (k == 0) NCCLCHK(ncclRecv(stage, (size_t)(row_bytes(L) * L.h), ncclUint8, peers[0], s.comm, s.stream));
         HIPCHK(hipStreamSynchronize(s.stream));  // block k is in slot k % 2
         if (k + 1 < peers.size()) {
             life_layout Ln;
             CHK(layout_of(peers[k + 1], &Ln));
-            NCCLCHK(ncclRecv(stage + ((k + 1) % 2) * slot, (size_t)(Ln.w * Ln.h * bpc), ncclUint8, peers[k + 1],
+            NCCLCHK(ncclRecv(stage + ((k + 1) % 2) * slot, (size_t)(row_bytes(Ln) * Ln.h), ncclUint8, peers[k + 1],
                              s.comm, s.stream));
         }
         CHK(place(L, stage + (k % 2) * slot));
@@ -1142,12 +1182,17 @@ extern "C" {
 
 int life_dev_gather(life_dev *d, uint8_t *grid) {
     if (!d) return LIFE_EINVAL;
-    return gather_impl(d, grid, 1);
+    return gather_impl(d, grid, Frame::DENSE);
 }
 
 int life_dev_gather_vtk(life_dev *d, char *body) {
     if (!d) return LIFE_EINVAL;
-    return gather_impl(d, reinterpret_cast<uint8_t *>(body), 2);
+    return gather_impl(d, reinterpret_cast<uint8_t *>(body), Frame::VTK);
+}
+
+int life_dev_gather_bits(life_dev *d, uint8_t *packed) {
+    if (!d) return LIFE_EINVAL;
+    return gather_impl(d, packed, Frame::BITS);
 }
 
 static int census(life_dev *d, unsigned long long out[2]) {

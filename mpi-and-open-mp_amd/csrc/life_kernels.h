@@ -144,6 +144,11 @@ hipError_t launch_export_block(const life_layout &L, const uint8_t *buf, uint8_t
 
 // The block's VTK cell data: '0'/'1' + '\n' per owned cell, rows of 2w bytes.
 hipError_t launch_vtk_block(const life_layout &L, const uint8_t *buf, uint8_t *out, hipStream_t s);
+// Packed rows (LIFEBITS: bit x & 7 of byte x >> 3) of a block starting at
+// global column x0: bits_row_bytes(L) bytes per row, the block's cells from
+// bit x0 & 7 of its first byte on.
+inline int64_t bits_row_bytes(const life_layout &L) { return ((L.x0 & 7) + L.w + 7) / 8; }
+hipError_t launch_bits_block(const life_layout &L, const uint8_t *buf, uint8_t *out, hipStream_t s);
 
 // Counter-based synthetic init of the owned cells (global indices).
 hipError_t launch_fill_random(const life_layout &L, int64_t nx, uint64_t key, uint32_t thr32,

@@ -1023,6 +1023,41 @@ __global__ void vtk_kernel(const uint8_t *buf, int64_t pitch, int64_t ya, int64_
     }
 }
 
+// Packed frame rows of a block (the driver's LIFEBITS checkpoint format:
+// cell x of a row at bit (x & 7) of byte (x >> 3)).  The block starts at
+// global column x0; with s = x0 & 7 its cells land at bits s.. of its first
+// output byte, so output byte j holds block cells 8j - s .. 8j - s + 7 (those
+// outside [0, w) are 0: the host ORs the bytes two blocks share).  One thread
+// per output byte; 2-D grid, y strides rows.  Bit encoding: the cells are
+// already little-endian bits, a funnel shift of two words.
+template <bool BIT>
+__global__ void bits_kernel(const uint8_t *buf, int64_t pitch, int64_t ya, int64_t xoff, int64_t w, int64_t h,
+                            int s, uint8_t *out, int64_t rb) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= rb) return;
+    const int64_t c0 = 8 * j - s;  // block cell of bit 0 of this byte (>= -7)
+    const uint32_t lo = c0 < 0 ? (uint32_t)(-c0) : 0u;                     // bits below: none
+    const uint32_t hi = w - c0 >= 8 ? 8u : (uint32_t)(w - c0);            // bits at and above: none
+    const uint32_t keep = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+    for (int64_t y = blockIdx.y; y < h; y += gridDim.y) {
+        const uint8_t *row = buf + (y + ya) * pitch + xoff;
+        uint32_t v;
+        if (BIT) {
+            const uint32_t *wd = reinterpret_cast<const uint32_t *>(row);
+            if (c0 < 0) {
+                v = wd[0] << lo;
+            } else {
+                const int64_t k = c0 >> 5;  // the next word is owned or x-apron / pitch padding: in-row
+                v = __builtin_amdgcn_alignbit(wd[k + 1], wd[k], (uint32_t)(c0 & 31));
+            }
+        } else {
+            v = 0;
+            for (uint32_t b = lo; b < hi; ++b) v |= (uint32_t)(row[c0 + b] & 1u) << b;
+        }
+        out[y * rb + j] = (uint8_t)(v & keep);
+    }
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
     z += 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -1543,6 +1578,17 @@ hipError_t launch_vtk_block(const life_layout &L, const uint8_t *buf, uint8_t *o
         vtk_kernel<true><<<grid, 256, 0, s>>>(buf, L.pitch, L.yapron, L.xoff, L.w, L.h, out);
     else
         vtk_kernel<false><<<grid, 256, 0, s>>>(buf, L.pitch, L.yapron, L.xoff, L.w, L.h, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_bits_block(const life_layout &L, const uint8_t *buf, uint8_t *out, hipStream_t s) {
+    const int sh = (int)(L.x0 & 7);
+    const int64_t rb = bits_row_bytes(L);
+    const dim3 grid(blocks_for(rb, 256), (unsigned)(L.h < 8192 ? L.h : 8192));
+    if (is_bit(L))
+        bits_kernel<true><<<grid, 256, 0, s>>>(buf, L.pitch, L.yapron, L.xoff, L.w, L.h, sh, out, rb);
+    else
+        bits_kernel<false><<<grid, 256, 0, s>>>(buf, L.pitch, L.yapron, L.xoff, L.w, L.h, sh, out, rb);
     return hipGetLastError();
 }
 

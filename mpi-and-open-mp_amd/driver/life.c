@@ -231,20 +231,14 @@ static int save_vtk(const char *path, int64_t nx, int64_t ny, const char *body) 
 
 /* Packed binary frame (extension, not in the reference): a text line
  * "LIFEBITS 1 <nx> <ny> <generation>\n", then ny rows of ceil(nx/8) bytes,
- * cell x of a row at bit (x & 7) of byte (x >> 3). */
-static int save_bits(const char *path, int64_t nx, int64_t ny, int64_t gen, const uint8_t *grid) {
+ * cell x of a row at bit (x & 7) of byte (x >> 3) -- packed on the device
+ * (life_dev_gather_bits), written as one block. */
+static int save_bits(const char *path, int64_t nx, int64_t ny, int64_t gen, const uint8_t *packed) {
     FILE *f = open_frame(path);
     if (!f) return LIFE_EIO;
     fprintf(f, "LIFEBITS 1 %lld %lld %lld\n", (long long)nx, (long long)ny, (long long)gen);
-    const int64_t rb = (nx + 7) / 8;
-    uint8_t *row = (uint8_t *)malloc((size_t)rb);
-    int ok = 1;
-    for (int64_t y = 0; y < ny && ok; y++) {
-        memset(row, 0, (size_t)rb);
-        for (int64_t x = 0; x < nx; x++) row[x >> 3] |= (uint8_t)((grid[y * nx + x] != 0) << (x & 7));
-        ok = fwrite(row, 1, (size_t)rb, f) == (size_t)rb;
-    }
-    free(row);
+    const size_t n = (size_t)(ny * ((nx + 7) / 8));
+    const int ok = fwrite(packed, 1, n, f) == n;
     return fclose(f) == 0 && ok ? LIFE_OK : LIFE_EIO;
 }
 
@@ -405,10 +399,10 @@ int main(int argc, char **argv) {
     }
     if (rc) die("create", rc);
     const int writer = !rank_mode || rank == root; /* the process that writes frames and prints */
-    uint8_t *grid = NULL; /* dense cells: bits frames */
+    uint8_t *grid = NULL; /* packed rows: bits frames */
     char *body = NULL;    /* VTK cell text */
     if (vtk && bits && writer) {
-        grid = (uint8_t *)calloc((size_t)(c.nx * c.ny), 1);
+        grid = (uint8_t *)calloc((size_t)(c.ny * ((c.nx + 7) / 8)), 1);
         if (!grid) die("host grid", LIFE_ENOMEM);
     }
     if (vtk && !bits && writer) {
@@ -437,7 +431,7 @@ int main(int argc, char **argv) {
     for (int64_t i = gen0; i < c.steps;) {
         const int save = vtk && i % c.save_steps == 0;
         if (save) { /* collect (blocking, every rank), then write it while the GPU steps on */
-            if ((rc = bits ? life_dev_gather(d, grid) : life_dev_gather_vtk(d, body))) die("gather", rc);
+            if ((rc = bits ? life_dev_gather_bits(d, grid) : life_dev_gather_vtk(d, body))) die("gather", rc);
             snprintf(path, sizeof path, bits ? "vtk/life_%06lld.bits" : "vtk/life_%06lld.vtk", (long long)i);
         }
         int64_t n = c.steps - i;

@@ -55,7 +55,7 @@ ABI_SYMBOLS = (
     "life_dev_step", "life_dev_gather", "life_dev_live_count", "life_dev_sync",
     "life_dev_layout", "life_dev_world", "life_dev_set_timing", "life_dev_kernel_stats",
     "life_tune", "life_tune_temporal", "life_dev_configure", "life_dev_kernel_work", "life_dev_checksum",
-    "life_dev_gather_vtk", "life_dev_destroy", "life_measure_copy", "life_dev_phase_stats",
+    "life_dev_gather_vtk", "life_dev_gather_bits", "life_dev_destroy", "life_measure_copy", "life_dev_phase_stats",
     "life_dev_barrier", "life_device_count", "life_dev_last_path",
 )
 PATHS = {0: "none", 1: "onegen", 2: "tiles", 3: "flow", 5: "small"}
@@ -136,6 +136,7 @@ def _lib():
         L.life_dev_step.argtypes = [vp, i64]
         L.life_dev_gather.argtypes = [vp, P(ctypes.c_uint8)]
         L.life_dev_gather_vtk.argtypes = [vp, ctypes.c_char_p]
+        L.life_dev_gather_bits.argtypes = [vp, ctypes.POINTER(ctypes.c_uint8)]
         L.life_dev_live_count.argtypes = [vp]
         L.life_dev_live_count.restype = i64
         L.life_dev_sync.argtypes = [vp]
@@ -315,6 +316,17 @@ class Life:
         body = ctypes.create_string_buffer(2 * self.nx * self.ny)
         _check(_lib().life_dev_gather_vtk(self._h, body), "gather_vtk")
         return vtk_header(self.nx, self.ny) + body.raw
+
+    def gather_bits(self, out: np.ndarray | None = None) -> np.ndarray:
+        """life_dev_gather_bits: packed rows (ny x ceil(nx/8) bytes, cell x at
+        bit x & 7 of byte x >> 3; == np.packbits(gather(), axis=1,
+        bitorder="little")), packed on the device."""
+        if out is None:
+            out = np.empty((self.ny, (self.nx + 7) // 8), dtype=np.uint8)
+        if out.shape != (self.ny, (self.nx + 7) // 8) or out.dtype != np.uint8 or not out.flags.c_contiguous:
+            raise ValueError("gather_bits: out must be a C-contiguous uint8 (ny, ceil(nx/8)) array")
+        _check(_lib().life_dev_gather_bits(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))), "gather_bits")
+        return out
 
     def live_count(self) -> int:
         return _check(_lib().life_dev_live_count(self._h), "live_count")

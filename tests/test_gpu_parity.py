@@ -294,3 +294,24 @@ def test_measure_copy_ceiling(gpu):
     (MI355X spec 8 TB/s; ~6.3 TB/s measured for a float4 copy)."""
     g = gpu.measure_copy(0, 1 << 30, 3)
     assert 2000.0 < g < 8000.0, g
+
+
+@pytest.mark.parametrize("kernel", ["byte", "bit"])
+@pytest.mark.parametrize("shards,dims,nx,ny", [
+    (1, (1, 1), 1000, 37), (1, (1, 1), 7, 5), (1, (1, 1), 4096, 300),
+    (6, (3, 2), 1000, 50), (3, (3, 1), 77, 20), (4, (2, 2), 1021, 64), (4, (1, 4), 96, 132), (2, (2, 1), 64, 40),
+])
+def test_gather_bits(gpu, oracle, kernel, shards, dims, nx, ny):
+    """life_dev_gather_bits (the driver's LIFEBITS frame body, packed on the
+    device) == np.packbits(gather(), little) -- including blocks whose x
+    start is not a multiple of 8, whose edge bytes two shards share."""
+    g0 = oracle.fill_random(nx, ny, seed=nx + shards, density=0.5)
+    with gpu.Life(nx, ny, shards=shards, kernel=kernel, dims=dims, transport=gpu.XPORT_LOCAL,
+                  small_grid=False) as life:
+        life.upload(g0)
+        life.step(3)
+        dense = life.gather()
+        np.testing.assert_array_equal(dense, oracle.life_run(g0, 3))
+        want = np.packbits(dense, axis=1, bitorder="little")
+        out = np.full((ny, (nx + 7) // 8), 0xA5, dtype=np.uint8)  # stale bytes must not survive
+        np.testing.assert_array_equal(life.gather_bits(out), want)
