@@ -472,7 +472,8 @@ int launch_tiles(life_dev *d, Shard &s, const life::TileRegion *r, int nreg, int
         if (!t) return rc;
         HIPCHK(hipEventRecord(t->a, st));
     }
-    HIPCHK(life::launch_tstep(s.lay, in, out, r, nreg, m, wrap_of(d), st));
+    double valu = 0.0;
+    HIPCHK(life::launch_tstep(s.lay, in, out, r, nreg, m, wrap_of(d), st, &valu));
     if (t) {
         HIPCHK(hipEventRecord(t->b, st));
         const life::TileGeom g = life::tile_geom(s.lay, m);
@@ -487,9 +488,8 @@ int launch_tiles(life_dev *d, Shard &s, const life::TileRegion *r, int nreg, int
                 d->acc_bytes += cells * (s.lay.kernel == LIFE_KERNEL_BIT ? 0.25 : 2.0);
                 d->acc_updates += cells * (double)m;
             }
-            const double tiles = (double)(r[k].tx1 - r[k].tx0) * (double)(r[k].ty1 - r[k].ty0);
-            d->acc_valu += tiles * 64.0 * life::tstep_valu_per_tile_lane(m, s.lay.kernel == LIFE_KERNEL_BYTE);
         }
+        d->acc_valu += valu;  // as tiled: tiles, banded items, half-height tail tiles
     }
     return LIFE_OK;
 }

@@ -57,8 +57,13 @@ struct TileRegion {
 };
 struct TileGeom {
     int64_t words, rows, ntx, nty;
+    int gsh;       // < 6: tile column bcol runs as bands of 2^gsh lanes (64 >> gsh tile rows per workgroup)
+    int64_t bcol;  // the banded column (ntx - 1), -1 without banding
 };
 TileGeom tile_geom(const life_layout &L, int m);
+// workgroups (items) one launch of region r takes: its full tiles, plus its
+// banded items when it holds the banded column
+int64_t region_items(const TileGeom &g, const TileRegion &r);
 int tile_ghost(const life_layout &L, int m);  // ghost rows per window end: m (bit) or K (byte)
 // Rows a temporally blocked buffer is allocated beyond its layout's `rows`:
 // the last tile's window (<= 8 waves x 96 rows) may read past the bottom
@@ -77,9 +82,11 @@ bool flow_ok(const life_layout &L, int m);
 int flow_slots(const life_layout &L);  // resident workgroups of L's dataflow kernel on this device
 hipError_t launch_tflow(const life_layout &L, const uint8_t *in, uint8_t *out, int m, int64_t passes,
                         unsigned int *head, unsigned int *done, Wrap wrap, int flow, hipStream_t s);
-// Up to 4 disjoint tile regions in one launch.
+// Up to 4 disjoint tile regions in one launch; *valu_lane_ops (optional):
+// the modelled VALU lane-ops of the launch as tiled (tstep_valu_per_tile_lane).
 hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, const TileRegion *r, int nreg,
-                        int m, Wrap wrap, hipStream_t s);
+                        int m, Wrap wrap, hipStream_t s,
+                        double *valu_lane_ops = nullptr);
 int temporal_rows(bool bit);      // register rows per wave (32/40/48/56/64/96)
 // VALU instructions the lanes at one lane position of a tile's waves issue
 // for m generations (the op-count model of life_kernels.hip tstep_kernel,

@@ -253,7 +253,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs a) {
 //  * tflow_kernel: every pass of a step call on a single wrapped shard in
 //    one persistent launch, tiles handed from pass to pass (LIFE_OPT_FLOW).
 
-constexpr int kStackWaves = 8;  // tstep: waves per workgroup (2 per SIMD)
+constexpr int kStackWaves = 8;  // waves per tile workgroup (2 per SIMD; 12 measured slower, profiles/r02/r2w)
 struct TArgs {
     const uint8_t *in;
     uint8_t *out;
@@ -262,6 +262,17 @@ struct TArgs {
     // partitioned shard); workgroup b belongs to the region with first[k] <= b
     int64_t tx0[kMaxRegions], tx1[kMaxRegions], ty0[kMaxRegions], ty1[kMaxRegions], first[kMaxRegions + 1];
     int32_t nreg, m;  // generations of the launch = ghost rows at each end of a window
+    // banded tile column (bit; tile_geom): gsh < 6 cuts the tiles of column
+    // bcol into bands of G = 2^gsh lanes, 64 / G tile rows per workgroup; a
+    // region whose tx1 == bcol + 1 lists its full tiles first, then its
+    // ceil((ty1 - ty0) / (64 / G)) banded items
+    int32_t gsh;
+    int64_t bcol;
+    // tail split (R = 48, one launch over the whole shard): workgroups
+    // >= half_first run half-height tiles (R / 2 rows per wave) over rows
+    // [half_y, h), half_ntx per tile row, so the last round of a launch is
+    // made of half-length items (launch_tstep)
+    int64_t half_first, half_y, half_ntx;
 };
 
 // Neighbour word from the left lane (DPP wave_shr:1, bound_ctrl: lane 0 reads
@@ -303,7 +314,8 @@ __device__ __forceinline__ void bit_hsum(uint32_t v, uint32_t &s0, uint32_t &s1)
 // loads / stores; byte: 16-B buffer loads / stores with the sc1 bit, one
 // buffer resource per row (a 65536^2 byte shard exceeds a resource's 32-bit
 // range).
-using Xch = uint32_t[2][kStackWaves][4][64];  // [parity][wave][top s0/s1, bottom s0/s1][lane]
+template <int NW>
+using Xch = uint32_t[2][NW][4][64];  // [parity][wave][top s0/s1, bottom s0/s1][lane]
 
 constexpr int kSc1 = 16;                  // buffer cache policy: sc1 (gfx94x/gfx950 CPol::SC1)
 constexpr int kRsrcFlags = 0x00020000;    // buffer resource dword 3 (gfx9 raw buffer, 32-bit data format)
@@ -320,11 +332,19 @@ __device__ __forceinline__ void store16_sc1(__amdgpu_buffer_rsrc_t rs, uint32_t 
     __builtin_amdgcn_raw_buffer_store_b128(t, rs, (int)off, 0, kSc1);
 }
 
-template <bool BYTE, int R, int GK, bool WRAPX, bool WRAPY, int FLOW>
+// Banded tiles (bit): a tile column that owns o <= 30 words (the last one:
+// W = 62 (ntx - 1) + o) wastes most of a 64-lane tile.  With gsh < 6 the wave
+// is cut into groups of G = 2^gsh lanes (1 ghost + o owned + ghost words),
+// group g holding tile row ty + g of that column: one workgroup carries nb <=
+// 64 / G tile rows ("bands").  The neighbour words a group's edge lanes fetch
+// come from the adjacent group: garbage, exactly as a tile's lanes 0 / 63
+// read beyond the tile, absorbed by the ghost lanes (<= m <= 31 bits).  Only
+// the loads and stores differ (per-lane rows); the generation loop is the
+// tile's.  gsh = 6: an ordinary tile (nb = 1).
+template <bool BYTE, int R, int GK, bool WRAPX, bool WRAPY, int FLOW, int NW, bool BAND = false>
 __device__ __forceinline__ void tile_body(const TArgs &a, const uint8_t *in, uint8_t *out, int64_t tx, int64_t ty,
-                                          Xch &xch) {
+                                          Xch<NW> &xch, int gsh = 6, int nb = 1, int64_t ybase = 0) {
     static_assert(R >= 3 && GK >= 0 && GK <= 32, "window");
-    constexpr int NW = kStackWaves;
     // the window's ghost rows at each end: GK, or (GK = 0) the launch's
     // generations m <= 32 (checked on the host); after m generations rows
     // [ghost, NW*R - ghost) are exact.  The byte tiles keep a compile-time
@@ -337,7 +357,12 @@ __device__ __forceinline__ void tile_body(const TArgs &a, const uint8_t *in, uin
     const int laddr = ((lane - 1) & 63) << 2;
     // wave index: uniform, so every row address below is scalar (SALU) math
     const int wi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t j = tx * 62 + lane - 1;  // word column of this lane
+    // a separate instance: a runtime switch in the one body cost the ordinary
+    // tiles 5-12 % (profiles/r02/r2w: w8_b0 vs r2v)
+    constexpr bool banded = BAND && !BYTE;
+    const int gl = banded ? lane >> gsh : 0;                  // this lane's band (tile row ty + gl)
+    const int pin = banded ? lane & ((1 << gsh) - 1) : lane;  // lane within its group
+    const int64_t j = tx * 62 + pin - 1;                      // word column of this lane
     int64_t jl;
     if (WRAPX) {
         jl = j % a.W;
@@ -346,19 +371,41 @@ __device__ __forceinline__ void tile_body(const TArgs &a, const uint8_t *in, uin
         jl = j > a.W ? a.W : j;  // words -1 .. W hold cells/apron; beyond: clamp (never stored)
     }
     const uint32_t voff = (uint32_t)(a.xoff + (BYTE ? 32 : 4) * jl);
-    const int64_t y0 = ty * T - K + (int64_t)wi * R;  // owned row of register row 0 (>= -K)
+    const int64_t y0 = ybase + ty * T - K + (int64_t)wi * R;  // owned row of register row 0 (>= -K)
     // Row pointers are walked: with a periodic y axis the walk wraps at h;
     // with an apron the last tile's window may run past the apron row h+K-1
     // into the allocation slack below the buffer (kTemporalSlackRows; those
     // rows are never stored).
     const uint8_t *row0 = in + a.ya * a.pitch;  // owned row 0
+    uint32_t v[R];
+    if (banded) {
+        // per-lane rows: band gl (lanes of bands >= nb load band nb - 1 and store nothing)
+        int64_t y = y0 + (int64_t)(gl < nb ? gl : nb - 1) * T;
+        if (WRAPY) {
+            y %= a.h;
+            if (y < 0) y += a.h;
+        }
+        const uint8_t *p = row0 + y * a.pitch;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            v[r] = FLOW ? __hip_atomic_load(reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(p) + voff),
+                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                        : *reinterpret_cast<const uint32_t *>(p + voff);
+            ++y;
+            if (WRAPY && y == a.h) {
+                y = 0;
+                p = row0;
+            } else {
+                p += a.pitch;
+            }
+        }
+    } else {
     int64_t y = y0;
     if (WRAPY) {
         y %= a.h;
         if (y < 0) y += a.h;
     }
     const uint8_t *p = row0 + y * a.pitch;
-    uint32_t v[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         if (BYTE && FLOW) {
@@ -380,6 +427,7 @@ __device__ __forceinline__ void tile_body(const TArgs &a, const uint8_t *in, uin
         } else {
             p += a.pitch;
         }
+    }
     }
     auto hsum = [&](uint32_t x, uint32_t &s0, uint32_t &s1, uint32_t &L) {
         if (DRIFT) {
@@ -434,9 +482,30 @@ __device__ __forceinline__ void tile_body(const TArgs &a, const uint8_t *in, uin
         v[R - 1] = BitEnc::rule1(p0, p1, b0, b1, d0, d1, bL);
         v[0] = BitEnc::rule1(a0, a1, t0, t1, h10, h11, tL);
     }
+    // window rows [K, NW*R - K) are the tile's owned rows [ty*T, ty*T + T);
+    // this wave's share of them (a half-height tile's ghost rows may span more
+    // than one wave: K > R)
+    const int r0 = min(max(K - wi * R, 0), R), r1 = min(max(NW * R - K - wi * R, 0), R);
+    if (banded) {
+        const int G = 1 << gsh;
+        const bool st = pin >= 1 && pin <= G - 2 && j < a.W && gl < nb;
+        const int64_t yb = y0 + (int64_t)(gl < nb ? gl : 0) * T;  // this lane's band
+        uint8_t *q = out + (a.ya + yb + r0) * a.pitch + voff;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (r < r0 || r >= r1) continue;
+            if (st && yb + r < a.h) {
+                if (FLOW == 1)
+                    __hip_atomic_store(reinterpret_cast<uint32_t *>(q), v[r], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                else
+                    *reinterpret_cast<uint32_t *>(q) = v[r];
+            }
+            q += a.pitch;
+        }
+        return;
+    }
     const bool st = lane >= 1 && lane <= 62 && j < a.W;
-    // window rows [K, NW*R - K) are the tile's owned rows [ty*T, ty*T + T)
-    const int r0 = wi == 0 ? K : 0, r1 = wi == NW - 1 ? R - K : R;
     uint8_t *q = out + (a.ya + y0 + r0) * a.pitch + voff;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -461,18 +530,32 @@ __device__ __forceinline__ void tile_body(const TArgs &a, const uint8_t *in, uin
     }
 }
 
-template <bool BYTE, int R, int GK, bool WRAPX, bool WRAPY>
-__global__ __launch_bounds__(64 * kStackWaves, 4) void tstep_kernel(TArgs a) {  // 4 waves/SIMD: 2 tiles per CU
-    __shared__ Xch xch;
-    const int64_t nwg = a.first[a.nreg];
-    if ((int64_t)blockIdx.x >= nwg) return;  // whole workgroup
+template <bool BYTE, int R, int GK, bool WRAPX, bool WRAPY, int NW>
+__global__ __launch_bounds__(64 * NW, 4) void tstep_kernel(TArgs a) {
+    __shared__ Xch<NW> xch;
     const int64_t wg = blockIdx.x;
+    if (R == 48 && a.half_first > 0 && wg >= a.half_first) {
+        const int64_t i = wg - a.half_first;
+        tile_body<BYTE, R / 2, GK, WRAPX, WRAPY, 0, NW>(a, a.in, a.out, i % a.half_ntx, i / a.half_ntx, xch, 6, 1,
+                                                        a.half_y);
+        return;
+    }
+    const int64_t nwg = a.first[a.nreg];
+    if (wg >= nwg) return;  // whole workgroup
     int k = 0;
     while (k + 1 < a.nreg && wg >= a.first[k + 1]) ++k;
     const int64_t wr = wg - a.first[k];
-    const int64_t ntx = a.tx1[k] - a.tx0[k];
-    const int64_t tx = a.tx0[k] + wr % ntx, ty = a.ty0[k] + wr / ntx;
-    tile_body<BYTE, R, GK, WRAPX, WRAPY, 0>(a, a.in, a.out, tx, ty, xch);
+    const bool bands = a.gsh < 6 && a.tx1[k] == a.bcol + 1;
+    const int64_t ntx = a.tx1[k] - a.tx0[k] - (bands ? 1 : 0);
+    const int64_t nfull = ntx * (a.ty1[k] - a.ty0[k]);
+    if (wr < nfull) {
+        const int64_t tx = a.tx0[k] + wr % ntx, ty = a.ty0[k] + wr / ntx;
+        tile_body<BYTE, R, GK, WRAPX, WRAPY, 0, NW>(a, a.in, a.out, tx, ty, xch);
+    } else if (!BYTE) {
+        const int64_t B = 64 >> a.gsh, ty = a.ty0[k] + (wr - nfull) * B;
+        const int nb = (int)(a.ty1[k] - ty < B ? a.ty1[k] - ty : B);
+        tile_body<BYTE, R, GK, WRAPX, WRAPY, 0, NW, true>(a, a.in, a.out, a.bcol, ty, xch, a.gsh, nb);
+    }
 }
 
 // tflow_kernel: `passes` launches of the bit tiles (m generations each, both
@@ -499,10 +582,13 @@ struct FArgs {
     unsigned int *done;              // per tile: passes completed (zeroed before the launch)
 };
 
-// bit: 3 tiles per CU (80 VGPRs); byte: 2 (its 92 VGPRs)
-template <bool BYTE, int R, int GK, bool WRAPX, bool WRAPY, int FLOW>
-__global__ __launch_bounds__(64 * kStackWaves, BYTE ? 4 : 6) void tflow_kernel(FArgs f) {
-    __shared__ Xch xch;
+// bit: 3 tiles per CU (80 VGPRs); byte: 2 (its 92 VGPRs).  No banded column
+// here: the banded items in this loop cost the ordinary tiles 2.5 % (code
+// size in the persistent loop; profiles/r02/r2x: b0 / b1 vs base), more than
+// they save.
+template <bool BYTE, int R, int GK, bool WRAPX, bool WRAPY, int FLOW, int NW>
+__global__ __launch_bounds__(64 * NW, BYTE ? 4 : 6) void tflow_kernel(FArgs f) {
+    __shared__ Xch<NW> xch;
     __shared__ unsigned int item_sh;
     const TArgs &a = f.t;
     const int64_t tiles = f.ntx * f.nty;
@@ -566,7 +652,7 @@ __global__ __launch_bounds__(64 * kStackWaves, BYTE ? 4 : 6) void tflow_kernel(F
         __syncthreads();
         const uint8_t *in = (p & 1) ? a.out : a.in;
         uint8_t *out = const_cast<uint8_t *>((p & 1) ? a.in : a.out);
-        tile_body<BYTE, R, GK, WRAPX, WRAPY, FLOW>(a, in, out, tx, ty, xch);
+        tile_body<BYTE, R, GK, WRAPX, WRAPY, FLOW, NW>(a, in, out, tx, ty, xch);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
         __syncthreads();
         prev_flag = f.done + ty * f.ntx + tx;
@@ -1178,6 +1264,7 @@ int temporal_rows(bool bit) {
     return temporal_rows_ok(nr) ? nr : (bit ? 48 : 32);
 }
 
+
 // Per register row and generation: bit_hsum = 1 DPP move + 2 v_alignbit + 2
 // v_bitop3 (+ 1 ds_bpermute on the LDS pipe), rule1 = 8 v_bitop3: 13; the
 // byte tiles run the drifting frame (12) and add pack (8 v_dot4 + 3 shifts)
@@ -1256,17 +1343,17 @@ hipError_t launch_step(const life_layout &L, const uint8_t *in, uint8_t *out, ui
 }
 
 namespace {
-template <bool BYTE, int R, int GK>
+template <bool BYTE, int R, int GK, int NW = kStackWaves>
 hipError_t launch_t(const TArgs &a, Wrap wrap, unsigned grid, hipStream_t s) {
-    constexpr unsigned kThreads = 64 * kStackWaves;
+    constexpr unsigned kThreads = 64 * NW;
     if (wrap.x && wrap.y)
-        tstep_kernel<BYTE, R, GK, true, true><<<grid, kThreads, 0, s>>>(a);
+        tstep_kernel<BYTE, R, GK, true, true, NW><<<grid, kThreads, 0, s>>>(a);
     else if (wrap.x)
-        tstep_kernel<BYTE, R, GK, true, false><<<grid, kThreads, 0, s>>>(a);
+        tstep_kernel<BYTE, R, GK, true, false, NW><<<grid, kThreads, 0, s>>>(a);
     else if (wrap.y)
-        tstep_kernel<BYTE, R, GK, false, true><<<grid, kThreads, 0, s>>>(a);
+        tstep_kernel<BYTE, R, GK, false, true, NW><<<grid, kThreads, 0, s>>>(a);
     else
-        tstep_kernel<BYTE, R, GK, false, false><<<grid, kThreads, 0, s>>>(a);
+        tstep_kernel<BYTE, R, GK, false, false, NW><<<grid, kThreads, 0, s>>>(a);
     return hipGetLastError();
 }
 
@@ -1287,17 +1374,67 @@ int tile_ghost(const life_layout &L, int m) { return is_bit(L) ? m : L.generatio
 
 
 
+// LIFE_BANDS=0: no banded tile column (A/B knob)
+static bool bands_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("LIFE_BANDS");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return on;
+}
+
 TileGeom tile_geom(const life_layout &L, int m) {
     TileGeom g;
     g.words = 62;
     g.rows = (int64_t)kStackWaves * temporal_rows(is_bit(L)) - 2 * (int64_t)tile_ghost(L, m);
-    g.ntx = ((L.w + 31) / 32 + g.words - 1) / g.words;
+    const int64_t W = (L.w + 31) / 32;
+    g.ntx = (W + g.words - 1) / g.words;
     g.nty = (L.h + g.rows - 1) / g.rows;
+    // the last tile column owns o words: bands of G >= o + 2 lanes when G <= 32
+    // (65536^2: o = 2, G = 4, 16 tile rows per workgroup instead of 1)
+    const int64_t o = W - g.words * (g.ntx - 1);
+    int gsh = 2;
+    while ((1 << gsh) < o + 2) ++gsh;
+    g.gsh = is_bit(L) && bands_enabled() && gsh <= 5 ? gsh : 6;
+    g.bcol = g.gsh < 6 ? g.ntx - 1 : -1;
     return g;
 }
 
+// LIFE_TAIL_SPLIT=0: no half-height tail tiles (A/B knob)
+static bool tail_split_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("LIFE_TAIL_SPLIT");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return on;
+}
+
+// resident workgroups of the R = 48 tiles of an encoding on this device
+// (occupancy, once): bit 3 per CU, byte 2
+static int slots_of(const void *fn) {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 64 * kStackWaves, 0) != hipSuccess)
+        return 0;
+    return cus * per;
+}
+static int tstep_slots(bool bit) {
+    static const int nbit = slots_of((const void *)tstep_kernel<false, 48, 0, true, true, kStackWaves>);
+    static const int nbyte = slots_of((const void *)tstep_kernel<true, 48, 32, true, true, kStackWaves>);
+    return bit ? nbit : nbyte;
+}
+
+int64_t region_items(const TileGeom &g, const TileRegion &r) {
+    if (r.tx1 <= r.tx0 || r.ty1 <= r.ty0) return 0;
+    if (g.gsh >= 6 || r.tx1 != g.bcol + 1) return (r.tx1 - r.tx0) * (r.ty1 - r.ty0);
+    const int64_t B = 64 >> g.gsh;
+    return (r.tx1 - r.tx0 - 1) * (r.ty1 - r.ty0) + (r.ty1 - r.ty0 + B - 1) / B;
+}
+
 hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, const TileRegion *r, int nreg,
-                        int m, Wrap wrap, hipStream_t s) {
+                        int m, Wrap wrap, hipStream_t s,
+                        double *valu_lane_ops) {
     const int K = L.generations_per_exchange;
     // m <= 32: the tile's edge lanes absorb at most 32 wrong bits; m <= the
     // apron depth a partitioned axis provides
@@ -1316,6 +1453,9 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
     a.m = m;
     a.nreg = 0;
     a.first[0] = 0;
+    const TileGeom g = tile_geom(L, m);
+    a.gsh = (int32_t)g.gsh;
+    a.bcol = g.bcol;
     for (int k = 0; k < nreg; k++) {
         if (r[k].tx1 <= r[k].tx0 || r[k].ty1 <= r[k].ty0) continue;
         const int n = a.nreg++;
@@ -1323,10 +1463,45 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
         a.tx1[n] = r[k].tx1;
         a.ty0[n] = r[k].ty0;
         a.ty1[n] = r[k].ty1;
-        a.first[n + 1] = a.first[n] + (r[k].tx1 - r[k].tx0) * (r[k].ty1 - r[k].ty0);
+        a.first[n + 1] = a.first[n] + region_items(g, r[k]);
     }
     if (a.nreg == 0 || m <= 0) return hipSuccess;
-    const unsigned grid = (unsigned)a.first[a.nreg];  // one workgroup per tile
+    int64_t items = a.first[a.nreg];  // one workgroup per tile (or banded item)
+    a.half_first = a.half_y = a.half_ntx = 0;
+    if (is_bit(L) && temporal_rows(true) == 48 && a.nreg == 1 && a.tx0[0] == 0 && a.tx1[0] == g.ntx &&
+        a.ty0[0] == 0 && a.ty1[0] == g.nty && tail_split_enabled()) {
+        // The launch runs items / slots rounds of equal tiles; a last round
+        // under half full leaves most CUs idle for a whole tile time (bit
+        // 65536^2, 20 generations: 6315 items on 768 slots = 8.2 rounds).
+        // Measured (profiles/r02/r2z): bit 20-generation calls +1.5-2 %; the
+        // byte tiles (2 per CU, 32 ghost rows: a third of a half tile) lost
+        // 3-4 %, so they keep whole tiles.
+        // Re-tile the bottom q tile rows as half-height tiles (R = 24, one
+        // round's worth or more): they are dispatched last, so the final round
+        // is half-length items on every slot.
+        const int slots = tstep_slots(is_bit(L));
+        const int64_t T2 = (int64_t)kStackWaves * 24 - 2 * (int64_t)tile_ghost(L, m);  // half tile: owned rows
+        const int64_t rem = slots > 0 ? items % slots : 0;
+        if (slots > 0 && items > slots && rem != 0 && rem <= slots / 2) {
+            int64_t q = 1;
+            while (q < g.nty && ((q * g.rows + T2 - 1) / T2) * g.ntx < slots) ++q;
+            if (q < g.nty) {
+                a.ty1[0] = g.nty - q;
+                a.first[1] = region_items(g, TileRegion{0, g.ntx, 0, a.ty1[0]});
+                a.half_first = a.first[1];
+                a.half_y = a.ty1[0] * g.rows;
+                a.half_ntx = g.ntx;
+                items = a.half_first + ((L.h - a.half_y + T2 - 1) / T2) * g.ntx;
+            }
+        }
+    }
+    if (valu_lane_ops) {
+        const bool byte = !is_bit(L);
+        *valu_lane_ops = (double)(a.half_first > 0 ? a.half_first : items) * 64.0 * tstep_valu_per_tile_lane(m, byte);
+        if (a.half_first > 0)  // half tiles: R / 2 register rows per wave
+            *valu_lane_ops += (double)(items - a.half_first) * 64.0 * 0.5 * tstep_valu_per_tile_lane(m, byte);
+    }
+    const unsigned grid = (unsigned)items;
     if (is_bit(L)) return launch_k<false, 0>(a, wrap, grid, s);
     return K == 16 ? launch_k<true, 16>(a, wrap, grid, s) : launch_k<true, 32>(a, wrap, grid, s);
 }
@@ -1334,9 +1509,9 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
 namespace {
 // Instances of the dataflow tiles: bit R = 40 / 48 (runtime ghost rows =
 // m), byte R = 48 with K = 16 / 32 ghost rows (compile-time, as tstep).
-template <bool BYTE, int R, int GK, int FLOW>
+template <bool BYTE, int R, int GK, int FLOW, int NW = kStackWaves>
 const void *flow_fn() {
-    return (const void *)tflow_kernel<BYTE, R, GK, true, true, FLOW>;
+    return (const void *)tflow_kernel<BYTE, R, GK, true, true, FLOW, NW>;
 }
 const void *flow_kernel_of(const life_layout &L, int flow) {
     const bool f2 = flow == 2;
@@ -1388,6 +1563,8 @@ hipError_t launch_tflow(const life_layout &L, const uint8_t *in, uint8_t *out, i
     f.t.h = L.h;
     f.t.ya = L.yapron;
     f.t.m = m;
+    f.t.gsh = 6;  // no banded column in the dataflow form
+    f.t.bcol = -1;
     f.ntx = g.ntx;
     f.nty = g.nty;
     f.items = passes * g.ntx * g.nty;

@@ -46,6 +46,7 @@ OPT_SMALL_GRID, OPT_OVERLAP, OPT_SMALL_WINDOW, OPT_BLOCK_GENS, OPT_LOOPBACK, OPT
 TEMPORAL_DEPTH = {"bit": 32, "byte": 32}
 BLOCK_GENS = {"bit": 20, "byte": 32}  # tiles: default generations per launch at most (LIFE_OPT_BLOCK_GENS)
 TEMPORAL_ROWS = {"bit": 48, "byte": 48}  # default register rows per wave of the temporal tiles
+TILE_WAVES = {"bit": 8, "byte": 8}  # waves per tile workgroup (window = waves x rows)
 
 # Every symbol include/life_mi355x.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = (

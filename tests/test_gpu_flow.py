@@ -14,8 +14,9 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 # nx (multiple of 32: x wraps inside the words), ny, generations, m
+# (2048 x 8000: 24 tile rows, the rotation wraps several times per call)
 CASES = [(2048, 1000, 47, 20), (1024, 3000, 64, 16), (4096, 1100, 33, 10), (1984, 700, 90, 32), (64, 900, 25, 8),
-         (2080, 2000, 61, 12), (32, 2048, 40, 20)]
+         (2080, 2000, 61, 12), (32, 2048, 40, 20), (2048, 8000, 41, 20)]
 
 
 @pytest.mark.parametrize("flow", [1, 2])

@@ -114,3 +114,30 @@ def test_c5_weak_scaling_shape_8_shards(gpu):
         life.fill_random(3, 0.5)
         life.step(gens)
         assert (life.checksum(), life.live_count()) == got
+
+
+@pytest.mark.parametrize("kernel,nx,ny,gens,bmax", [
+    ("bit", 65536, 65536, 20, 20), ("bit", 16384, 32768, 20, 20), ("bit", 16384, 32768, 13, 20),
+    ("bit", 65536, 65536, 7, 20), ("bit", 16384, 32768, 32, 32), ("bit", 16384, 32768, 28, 32),
+    ("byte", 32768, 32768, 32, 32), ("byte", 32768, 32768, 9, 32)])
+def test_single_launch_tail_split(gpu, kernel, nx, ny, gens, bmax):
+    """A one-launch step call on one shard (the driver's 20-generation run):
+    the bottom tile rows are re-tiled as half-height tiles when the last round
+    of the launch would be under half full (life_kernels.hip launch_tstep;
+    65536^2: 6315 items on 768 slots), and the last tile column runs as bands
+    of 4 lanes.  Checked against the same grid as two LOCAL row strips (the
+    partitioned ring + interior launches, neither split nor whole-grid).
+    Half-height tiles hold 24 rows per wave: with more than 24 ghost rows (bit
+    m > 24) the ghost rows span two waves.  (Byte: whole tiles, checked the
+    same way.)"""
+    with gpu.Life(nx, ny, kernel=kernel, flow=0) as life:
+        life.configure(gpu.OPT_BLOCK_GENS, bmax)
+        life.fill_random(3, 0.5)
+        life.set_timing(True)
+        life.step(gens)
+        assert life.last_path() == "tiles"
+        got = (life.checksum(), life.live_count())
+    with gpu.Life(nx, ny, shards=2, dims=(1, 2), kernel=kernel, transport=gpu.XPORT_LOCAL) as life:
+        life.fill_random(3, 0.5)
+        life.step(gens)
+        assert (life.checksum(), life.live_count()) == got

@@ -3,6 +3,8 @@
 Bit-exact on every cell.  The oracle restates 3-life/life2d.c:104-130 and is
 itself pinned to the reference (tests/test_oracle.py).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -108,16 +110,21 @@ def test_timing_stats(gpu, kernel, nx, gens, flow):
         assert n * b == pytest.approx(nx * 4096 * launches * (0.25 if kernel == "bit" else 2.0))
         assert n * upd == pytest.approx(nx * 4096 * gens)
         assert (valu > 0) == temporal
-        if temporal:  # 3 x ceil(4096 / (8 waves x R rows - 2m)) tiles of 62 words, 64 lanes;
+        if temporal:  # 3 x ceil(4096 / (NW waves x R rows - 2m)) tiles of 62 words, 64 lanes;
             # byte: + pack/unpack (35 ops per register row per launch)
-            R = gpu.TEMPORAL_ROWS[kernel]
+            R, NW = gpu.TEMPORAL_ROWS[kernel], gpu.TILE_WAVES[kernel]
             want = 0
             for m in sizes:
                 ghost = m if kernel == "bit" else K  # byte tiles: compile-time ghost depth K
-                tiles = 3 * -(-4096 // (8 * R - 2 * ghost))
+                nty = -(-4096 // (NW * R - 2 * ghost))
+                tiles = 3 * nty
+                if kernel == "bit" and not flow and os.environ.get("LIFE_BANDS", "1") != "0":
+                    # per-launch tiles, W = 128 words: the third tile column owns 4 words -> bands of 8 lanes, 8
+                    # tile rows per workgroup (life_kernels.hip tile_geom / region_items; not in the dataflow form)
+                    tiles = 2 * nty + -(-nty // 8)
                 # 13 VALU + 1 LDS per row; byte: drifting frame, 12 VALU + 1 LDS
                 per_row = (12 if kernel == "byte" else 13) * m + (35 if kernel == "byte" else 0)
-                want += tiles * 64 * 8 * R * per_row
+                want += tiles * 64 * NW * R * per_row
             assert n * valu == pytest.approx(want)
 
 
