@@ -268,11 +268,11 @@ struct TArgs {
     // ceil((ty1 - ty0) / (64 / G)) banded items
     int32_t gsh;
     int64_t bcol;
-    // tail split (R = 48, one launch over the whole shard): workgroups
+    // tail split (R = 48, one launch of one full-width region): workgroups
     // >= half_first run half-height tiles (R / 2 rows per wave) over rows
-    // [half_y, h), half_ntx per tile row, so the last round of a launch is
-    // made of half-length items (launch_tstep)
-    int64_t half_first, half_y, half_ntx;
+    // [half_y, half_yend), half_ntx per tile row, so the last round of a
+    // launch is made of half-length items (launch_tstep)
+    int64_t half_first, half_y, half_ntx, half_yend;
 };
 
 // Neighbour word from the left lane (DPP wave_shr:1, bound_ctrl: lane 0 reads
@@ -343,7 +343,8 @@ __device__ __forceinline__ void store16_sc1(__amdgpu_buffer_rsrc_t rs, uint32_t 
 // tile's.  gsh = 6: an ordinary tile (nb = 1).
 template <bool BYTE, int R, int GK, bool WRAPX, bool WRAPY, int FLOW, int NW, bool BAND = false>
 __device__ __forceinline__ void tile_body(const TArgs &a, const uint8_t *in, uint8_t *out, int64_t tx, int64_t ty,
-                                          Xch<NW> &xch, int gsh = 6, int nb = 1, int64_t ybase = 0) {
+                                          Xch<NW> &xch, int gsh = 6, int nb = 1, int64_t ybase = 0,
+                                          int64_t yend = -1) {
     static_assert(R >= 3 && GK >= 0 && GK <= 32, "window");
     // the window's ghost rows at each end: GK, or (GK = 0) the launch's
     // generations m <= 32 (checked on the host); after m generations rows
@@ -506,12 +507,13 @@ __device__ __forceinline__ void tile_body(const TArgs &a, const uint8_t *in, uin
         return;
     }
     const bool st = lane >= 1 && lane <= 62 && j < a.W;
+    const int64_t ylim = yend >= 0 ? yend : a.h;  // half tiles of a region stop at its last row
     uint8_t *q = out + (a.ya + y0 + r0) * a.pitch + voff;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         if (r < r0 || r >= r1) continue;
         if (DRIFT) v[r] = drift_realign(v[r], a.m);  // every lane: the bpermute reads lane + 1
-        if (st && y0 + r < a.h) {
+        if (st && y0 + r < ylim) {
             if (BYTE && FLOW == 1) {
                 const __amdgpu_buffer_rsrc_t rs = row_rsrc(q - voff, a.pitch);  // the row: uniform
                 store16_sc1(rs, voff, unpack_half(v[r], 0));
@@ -537,7 +539,7 @@ __global__ __launch_bounds__(64 * NW, 4) void tstep_kernel(TArgs a) {
     if (R == 48 && a.half_first > 0 && wg >= a.half_first) {
         const int64_t i = wg - a.half_first;
         tile_body<BYTE, R / 2, GK, WRAPX, WRAPY, 0, NW>(a, a.in, a.out, i % a.half_ntx, i / a.half_ntx, xch, 6, 1,
-                                                        a.half_y);
+                                                        a.half_y, a.half_yend);
         return;
     }
     const int64_t nwg = a.first[a.nreg];
@@ -1467,9 +1469,11 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
     }
     if (a.nreg == 0 || m <= 0) return hipSuccess;
     int64_t items = a.first[a.nreg];  // one workgroup per tile (or banded item)
-    a.half_first = a.half_y = a.half_ntx = 0;
+    a.half_first = a.half_y = a.half_ntx = a.half_yend = 0;
     if (is_bit(L) && temporal_rows(true) == 48 && a.nreg == 1 && a.tx0[0] == 0 && a.tx1[0] == g.ntx &&
-        a.ty0[0] == 0 && a.ty1[0] == g.nty && tail_split_enabled()) {
+        tail_split_enabled()) {
+        // one full-width region: the whole shard, or the interior of a row
+        // strip (rows [ra, rb) of tiles; the ring runs concurrently)
         // The launch runs items / slots rounds of equal tiles; a last round
         // under half full leaves most CUs idle for a whole tile time (bit
         // 65536^2, 20 generations: 6315 items on 768 slots = 8.2 rounds).
@@ -1482,16 +1486,18 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
         const int slots = tstep_slots(is_bit(L));
         const int64_t T2 = (int64_t)kStackWaves * 24 - 2 * (int64_t)tile_ghost(L, m);  // half tile: owned rows
         const int64_t rem = slots > 0 ? items % slots : 0;
+        const int64_t ty0 = a.ty0[0], ty1 = a.ty1[0], yend = std::min(ty1 * g.rows, L.h);
         if (slots > 0 && items > slots && rem != 0 && rem <= slots / 2) {
             int64_t q = 1;
-            while (q < g.nty && ((q * g.rows + T2 - 1) / T2) * g.ntx < slots) ++q;
-            if (q < g.nty) {
-                a.ty1[0] = g.nty - q;
-                a.first[1] = region_items(g, TileRegion{0, g.ntx, 0, a.ty1[0]});
+            while (q < ty1 - ty0 && ((q * g.rows + T2 - 1) / T2) * g.ntx < slots) ++q;
+            if (q < ty1 - ty0) {
+                a.ty1[0] = ty1 - q;
+                a.first[1] = region_items(g, TileRegion{0, g.ntx, ty0, a.ty1[0]});
                 a.half_first = a.first[1];
                 a.half_y = a.ty1[0] * g.rows;
+                a.half_yend = yend;
                 a.half_ntx = g.ntx;
-                items = a.half_first + ((L.h - a.half_y + T2 - 1) / T2) * g.ntx;
+                items = a.half_first + ((yend - a.half_y + T2 - 1) / T2) * g.ntx;
             }
         }
     }

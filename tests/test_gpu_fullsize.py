@@ -141,3 +141,20 @@ def test_single_launch_tail_split(gpu, kernel, nx, ny, gens, bmax):
         life.fill_random(3, 0.5)
         life.step(gens)
         assert (life.checksum(), life.live_count()) == got
+
+
+def test_row_strip_interior_tail_split(gpu):
+    """The interior launch of a row strip (one full-width region of tile rows
+    [ra, rb) while the ring runs concurrently) takes half-height tail tiles
+    too, which stop at the region's last row: two 16384 x 32768 strips, two
+    20-generation blocks, against the single-shard dataflow tiles."""
+    nx, ny, gens = 16384, 65536, 40
+    with gpu.Life(nx, ny, kernel="bit", flow=1) as life:
+        life.fill_random(4, 0.5)
+        life.step(gens)
+        assert life.last_path() == "flow"
+        want = (life.checksum(), life.live_count())
+    with gpu.Life(nx, ny, shards=2, dims=(1, 2), kernel="bit", transport=gpu.XPORT_LOCAL) as life:
+        life.fill_random(4, 0.5)
+        life.step(gens)
+        assert (life.checksum(), life.live_count()) == want
