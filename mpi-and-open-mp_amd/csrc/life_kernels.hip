@@ -359,7 +359,8 @@ __device__ __forceinline__ void tile_body(const TArgs &a, const uint8_t *in, uin
     // wave index: uniform, so every row address below is scalar (SALU) math
     const int wi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // a separate instance: a runtime switch in the one body cost the ordinary
-    // tiles 5-12 % (profiles/r02/r2w: w8_b0 vs r2v)
+    // tiles 5-12 % (profiles/r02/r2w: w8_b0 vs r2v).  Bit only: a byte BAND
+    // instance in the byte tiles cost them 7 % (profiles/r02/r3c)
     constexpr bool banded = BAND && !BYTE;
     const int gl = banded ? lane >> gsh : 0;                  // this lane's band (tile row ty + gl)
     const int pin = banded ? lane & ((1 << gsh) - 1) : lane;  // lane within its group
