@@ -510,16 +510,32 @@ __device__ __forceinline__ void tile_body(const TArgs &a, const uint8_t *in, uin
     const bool st = lane >= 1 && lane <= 62 && j < a.W;
     const int64_t ylim = yend >= 0 ? yend : a.h;  // half tiles of a region stop at its last row
     uint8_t *q = out + (a.ya + y0 + r0) * a.pitch + voff;
+    // Byte write-through (FLOW 1) stores are not merged in L2, so each store
+    // instruction covers whole lines: lane l writes bytes [16 l, 16 l + 16) and
+    // [1024 + 16 l, ...) of the tile's 64-word span -- half (l & 1) of the
+    // words of lanes l >> 1 and 32 + (l >> 1), fetched by two ds_bpermute.
+    // (Lane-major 2 x 16 B per lane wrote every line twice: WRITE_SIZE 2x the
+    // per-launch tiles', profiles/r02/r3j.)
+    const int sa = lane >> 1, sb = 32 + (lane >> 1);  // source lanes
+    const bool st_a = sa >= 1 && sa <= 62 && tx * 62 + sa - 1 < a.W;
+    const bool st_b = sb >= 1 && sb <= 62 && tx * 62 + sb - 1 < a.W;
+    const uint32_t vbase = (uint32_t)(a.xoff + 32 * (tx * 62 - 1)) + 16u * (uint32_t)lane;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         if (r < r0 || r >= r1) continue;
         if (DRIFT) v[r] = drift_realign(v[r], a.m);  // every lane: the bpermute reads lane + 1
-        if (st && y0 + r < ylim) {
-            if (BYTE && FLOW == 1) {
+        if (BYTE && FLOW == 1) {
+            const uint32_t wa = bperm(sa << 2, v[r]), wb = bperm(sb << 2, v[r]);  // every lane
+            if (y0 + r < ylim) {
                 const __amdgpu_buffer_rsrc_t rs = row_rsrc(q - voff, a.pitch);  // the row: uniform
-                store16_sc1(rs, voff, unpack_half(v[r], 0));
-                store16_sc1(rs, voff + 16, unpack_half(v[r], 1));
-            } else if (BYTE) {
+                if (st_a) store16_sc1(rs, vbase, unpack_half(wa, lane & 1));
+                if (st_b) store16_sc1(rs, vbase + 1024u, unpack_half(wb, lane & 1));
+            }
+            q += a.pitch;
+            continue;
+        }
+        if (st && y0 + r < ylim) {
+            if (BYTE) {
                 uint4 *o = reinterpret_cast<uint4 *>(q);
                 o[0] = unpack_half(v[r], 0);
                 o[1] = unpack_half(v[r], 1);
