@@ -107,6 +107,12 @@ __device__ __forceinline__ uint32_t pack32(uint4 lo, uint4 hi) {
     const uint32_t b1 = __builtin_amdgcn_udot4(lo.z, W0, __builtin_amdgcn_udot4(lo.w, W1, b2 << 8, false), false);
     return __builtin_amdgcn_udot4(lo.x, W0, __builtin_amdgcn_udot4(lo.y, W1, b1 << 8, false), false);
 }
+// 16 byte cells (one 16-B load) -> 16 bits, cell k at bit k
+__device__ __forceinline__ uint32_t pack16(uint4 c) {
+    constexpr uint32_t W0 = 0x08040201u, W1 = 0x80402010u;
+    const uint32_t b1 = __builtin_amdgcn_udot4(c.z, W0, __builtin_amdgcn_udot4(c.w, W1, 0u, false), false);
+    return __builtin_amdgcn_udot4(c.x, W0, __builtin_amdgcn_udot4(c.y, W1, b1 << 8, false), false);
+}
 __device__ __forceinline__ uint32_t unpack_nibble(uint32_t w, int k) {
     // cells 4k..4k+3 -> bytes 0..3 (bit j of the nibble lands on bit 8j)
     return __umul24(__builtin_amdgcn_ubfe(w, 4 * k, 4), 0x204081u) & 0x01010101u;

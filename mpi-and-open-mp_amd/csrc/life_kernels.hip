@@ -408,11 +408,26 @@ __device__ __forceinline__ void tile_body(const TArgs &a, const uint8_t *in, uin
         if (y < 0) y += a.h;
     }
     const uint8_t *p = row0 + y * a.pitch;
+    // Byte write-through hand-off (FLOW): line-contiguous sc1 loads, as the
+    // stores below -- lane l loads bytes 16 l.. and 1024 + 16 l.. of the tile
+    // span and packs each to 16 cells; lane s takes its word's halves from
+    // lanes 2 (s % 32) and 2 (s % 32) + 1 (low / high halves of their packed
+    // pair for s < 32 / s >= 32: one v_perm).  Lanes whose word wraps
+    // (WRAPX: word -1 or >= W) load it directly.  Beyond the row the buffer
+    // resource reads zeros.
+    const uint32_t lbase = (uint32_t)(a.xoff + 32 * (tx * 62 - 1)) + 16u * (uint32_t)lane;
+    const int g0 = 2 * (lane & 31);
+    const uint32_t psel = lane < 32 ? 0x05040100u : 0x07060302u;
+    const bool wrapped = WRAPX && (j < 0 || j >= a.W);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         if (BYTE && FLOW) {
             const __amdgpu_buffer_rsrc_t rs = row_rsrc(p, a.pitch);
-            v[r] = pack32(load16_sc1(rs, voff), load16_sc1(rs, voff + 16));
+            const uint32_t P = pack16(load16_sc1(rs, lbase)) | (pack16(load16_sc1(rs, lbase + 1024u)) << 16);
+            const uint32_t q0 = bperm(g0 << 2, P), q1 = bperm((g0 + 1) << 2, P);
+            uint32_t w = __builtin_amdgcn_perm(q1, q0, psel);
+            if (wrapped) w = pack32(load16_sc1(rs, voff), load16_sc1(rs, voff + 16));
+            v[r] = w;
         } else if (BYTE) {
             const uint4 *q = reinterpret_cast<const uint4 *>(p + voff);
             v[r] = pack32(q[0], q[1]);
