@@ -15,10 +15,13 @@ HBM before timing.
                   [--scaling weak|strong] [--size 65536]
                   [--workload random|p46gun_big] [--partition auto|cart|rows|cols]
 
-Partition (life_dims_choose): "auto" (weak default) cuts the global grid into
-row strips, dims {1, N} (the 1-D decomposition of 3-life/5-gather): per-GPU
-cost measured 0-6 % lower than 2-D blocks and every halo message contiguous;
-"cart" (strong default) is 6-cartesian's MPI_Dims_create {2,1} / {2,2} / {4,2}.
+Partition (life_dims_choose): "cart" (the default for both scalings) is
+6-cartesian's MPI_Dims_create {2,1} / {2,2} / {4,2} split of life_cart.c:117-124
+-- at N = 8 weak scaling that is the 262144 x 131072 global grid of
+BASELINE configs[4] / SURVEY 8(d) C5, four halo peers per GPU; "rows" /
+"auto" cut row strips {1, N} (the 1-D decomposition of 3-life/5-gather: two
+peers, contiguous messages; measured 0-6 % cheaper per GPU with LOCAL
+copies on one MI355X, not yet over xGMI), "cols" column strips.
 
 N > 1 runs one process per GPU under torch.distributed.run: torch.distributed
 (gloo) carries the bootstrap (RCCL unique id), the barriers and the
@@ -77,8 +80,8 @@ def parse():
                    help="block edge per GPU (weak) or global grid edge (strong)")
     p.add_argument("--workload", default="random", choices=["random", "p46gun_big"])
     p.add_argument("--partition", default=None, choices=["auto", "cart", "rows", "cols"],
-                   help="shard shape (life_dims_choose); default: cart (MPI_Dims_create, life_cart.c:117-118) "
-                        "for strong scaling, auto (row strips when each is >= 1024 rows tall) for weak")
+                   help="shard shape (life_dims_choose); default: cart (MPI_Dims_create, life_cart.c:117-118: "
+                        "configs[3]'s and configs[4]'s 2-D split); auto = row strips when each is >= 1024 rows tall")
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline sample budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -199,7 +202,7 @@ def main():
         dist.init_process_group("gloo")
     n_gpus = world if world > 1 else a.gpus
     strong = a.scaling == "strong"
-    partition = a.partition or ("cart" if strong else "auto")
+    partition = a.partition or "cart"
     grid = None
     if a.workload == "p46gun_big":
         _, _, grid = lm.load_cfg(os.path.join(ROOT, "tests", "golden", "cfg", "p46gun_big.cfg"))

@@ -144,7 +144,10 @@ const char *life_last_error(void); /* detail of the last LIFE_EHIP/ERCCL on this
  * device copies otherwise (e.g. several logical shards on one GPU). */
 int life_dev_create(int64_t nx, int64_t ny, int nshards, int kernel, life_dev **out);
 
-/* Same with every knob: dims (0,0 = dims_create), transport. */
+/* Same with every knob: dims (0,0 = dims_create), transport.  LIFE_XPORT_RCCL
+ * needs one device per shard and builds one communicator rank per shard with
+ * ncclCommInitAll -- a single shard included (a one-device communicator, so
+ * LIFE_OPT_LOOPBACK exercises this single-process RCCL path on one GPU). */
 int life_dev_create_ex(int64_t nx, int64_t ny, int nshards, int dims0, int dims1, int kernel,
                        int transport, life_dev **out);
 
@@ -267,6 +270,11 @@ int life_dev_set_timing(life_dev *d, int on);
  * stores; 2: plain stores + a release fence per tile; + 4: the byte
  * encoding too (default off, or LIFE_FLOW_BYTE=1).  Same results. */
 #define LIFE_OPT_FLOW 7
+/* LIFE_OPT_FLOW_CHUNK (default 0 = automatic): the dataflow launch's queue
+ * head is a 32-bit counter, so a step call's passes are split over several
+ * persistent launches, each with passes x tiles + resident workgroups below
+ * 2^31 pulls; a positive value caps the passes per launch further (tests). */
+#define LIFE_OPT_FLOW_CHUNK 8
 int life_dev_configure(life_dev *d, int option, int value);
 /* The kernel family that ran the bulk of the last life_dev_step call:
  * LIFE_PATH_ONEGEN (one generation per launch), _TILES (temporally blocked
@@ -307,7 +315,7 @@ int life_tune(int kernel, int rows, int depth);
 /* Temporal (generations_per_exchange = K > 1) tile height of encoding
  * `kernel` (-1: both): register rows per wave, 32/40/48/56/64/96; a tile is one
  * workgroup of 8 vertically stacked waves, 8*rows - 2K owned rows; 0 keeps
- * the current values (defaults bit 48, byte 32, by measurement);
+ * the current values (default 48 for both encodings, by measurement);
  * LIFE_TEMPORAL_ROWS / LIFE_TEMPORAL_ROWS_BYTE override at load time. */
 int life_tune_temporal(int kernel, int rows);
 

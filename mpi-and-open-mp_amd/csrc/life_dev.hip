@@ -19,7 +19,9 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <chrono>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -149,7 +151,8 @@ struct life_dev {
     bool loop = false;  // LIFE_OPT_LOOPBACK: the one shard exchanges both axes' halos with itself
     int last_path = LIFE_PATH_NONE;  // life_dev_last_path
     int flow = kEnvFlow;
-    bool flow_byte = kEnvFlowByte;  // the dataflow form for the byte encoding too (LIFE_OPT_FLOW value | 4)  // LIFE_OPT_FLOW: single-shard bit tiles as one persistent dataflow launch per
+    bool flow_byte = kEnvFlowByte;
+    int64_t flow_chunk = 0;  // LIFE_OPT_FLOW_CHUNK: passes per dataflow launch at most (0: automatic)  // the dataflow form for the byte encoding too (LIFE_OPT_FLOW value | 4)  // LIFE_OPT_FLOW: single-shard bit tiles as one persistent dataflow launch per
                           // step call (1: write-through hand-off, 2: plain stores + release; 0 off)
     std::vector<Shard> shards;
     double acc_ms = 0.0;
@@ -655,6 +658,44 @@ int generation(life_dev *d) {
     return LIFE_OK;
 }
 
+// Seconds a rank-mode collective may take before it is declared dead
+// (LIFE_COMM_TIMEOUT_S, default 600): a peer that died or never joined would
+// otherwise leave this rank spinning in an RCCL kernel forever.
+double comm_timeout_s() {
+    static const double t = [] {
+        const char *e = getenv("LIFE_COMM_TIMEOUT_S");
+        const double v = e ? atof(e) : 0.0;
+        return v > 0.0 ? v : 600.0;
+    }();
+    return t;
+}
+
+// hipStreamSynchronize with a deadline: polls the stream; on timeout aborts
+// the shard's communicator (which ends RCCL kernels stuck on a missing peer)
+// and fails with a message naming the operation.
+int bounded_sync(Shard &s, const char *what, int peer) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spin = 0;; ++spin) {
+        const hipError_t e = hipStreamQuery(s.stream);
+        if (e == hipSuccess) return LIFE_OK;
+        if (e != hipErrorNotReady) {
+            set_err("%s (peer %d): %s", what, peer, hipGetErrorString(e));
+            return LIFE_EHIP;
+        }
+        const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (dt > comm_timeout_s()) {
+            if (s.comm) {
+                (void)ncclCommAbort(s.comm);
+                s.comm = nullptr;
+            }
+            set_err("%s: rank %d waited %.0f s for peer %d (LIFE_COMM_TIMEOUT_S); communicator aborted", what,
+                    s.rank, dt, peer);
+            return LIFE_ERCCL;
+        }
+        if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(spin > 4096 ? 1000 : 50));
+    }
+}
+
 int create_common(life_dev *d, const std::vector<int> &ranks, const std::vector<int> &devices) {
     for (size_t i = 0; i < ranks.size(); i++) {
         d->shards.emplace_back();
@@ -718,7 +759,11 @@ int life_dev_create_ex(int64_t nx, int64_t ny, int nshards, int dims0, int dims1
     }
     d->transport = transport;
     int rc = create_common(d, ranks, devices);
-    if (rc == LIFE_OK && transport == LIFE_XPORT_RCCL && nshards > 1) {
+    // RCCL: one communicator rank per shard, all driven by this process
+    // (ncclCommInitAll; the halo phases group every shard's sends / recvs in
+    // one ncclGroupStart/End).  A single shard gets a one-device communicator
+    // too, so LIFE_OPT_LOOPBACK runs this exact path on a one-GPU box.
+    if (rc == LIFE_OK && transport == LIFE_XPORT_RCCL) {
         std::vector<ncclComm_t> comms(nshards);
         ncclResult_t r = ncclCommInitAll(comms.data(), nshards, devices.data());
         if (r != ncclSuccess) {
@@ -923,25 +968,36 @@ static int step_flow(life_dev *d, int64_t generations, int64_t *done) {
         s.flow_words = words;
     }
     HIPCHK(hipSetDevice(s.device));
-    TimedLaunch *t = nullptr;
-    if (d->timing) {
-        int rc;
-        t = timer_slot(s, &rc);
-        if (!t) return rc;
-        HIPCHK(hipEventRecord(t->a, s.stream));
+    // The queue head is a 32-bit counter every resident workgroup bumps once
+    // past the last item: split the passes so that items + grid stays below
+    // 2^31 per launch (life::flow_chunk_passes), flipping the buffer parity
+    // per chunk.
+    const int64_t tiles = g.ntx * g.nty;
+    const int64_t per = life::flow_chunk_passes(tiles, life::flow_slots(L), d->flow_chunk);
+    if (per < 1) return LIFE_OK;  // a grid too large for one pass per launch: per-launch tiles
+    for (int64_t left = passes; left > 0;) {
+        const int64_t n = std::min(left, per);
+        TimedLaunch *t = nullptr;
+        if (d->timing) {
+            int rc;
+            t = timer_slot(s, &rc);
+            if (!t) return rc;
+            HIPCHK(hipEventRecord(t->a, s.stream));
+        }
+        HIPCHK(life::launch_tflow(L, s.buf[s.cur], s.buf[s.cur ^ 1], m, n, s.flow, s.flow + 2, wrap_of(d),
+                                  d->flow, s.stream));
+        if (t) {
+            HIPCHK(hipEventRecord(t->b, s.stream));
+            t->launches = (int)n;  // stats: mean per pass
+            const double cells = (double)L.w * (double)L.h;
+            const bool byte = d->kernel == LIFE_KERNEL_BYTE;
+            d->acc_bytes += (double)n * cells * (byte ? 2.0 : 0.25);
+            d->acc_updates += (double)n * cells * (double)m;
+            d->acc_valu += (double)n * (double)tiles * 64.0 * life::tstep_valu_per_tile_lane(m, byte);
+        }
+        if (n & 1) s.cur ^= 1;
+        left -= n;
     }
-    HIPCHK(life::launch_tflow(L, s.buf[s.cur], s.buf[s.cur ^ 1], m, passes, s.flow, s.flow + 2, wrap_of(d),
-                                 d->flow, s.stream));
-    if (t) {
-        HIPCHK(hipEventRecord(t->b, s.stream));
-        t->launches = (int)passes;  // stats: mean per pass
-        const double cells = (double)L.w * (double)L.h;
-        const bool byte = d->kernel == LIFE_KERNEL_BYTE;
-        d->acc_bytes += (double)passes * cells * (byte ? 2.0 : 0.25);
-        d->acc_updates += (double)passes * cells * (double)m;
-        d->acc_valu += (double)passes * (double)(g.ntx * g.nty) * 64.0 * life::tstep_valu_per_tile_lane(m, byte);
-    }
-    if (passes & 1) s.cur ^= 1;
     s.flow_used = true;
     *done = passes * m;
     return LIFE_OK;
@@ -1010,7 +1066,7 @@ int life_dev_barrier(life_dev *d) {
                 // an all-reduce every rank must join: no rank leaves before all arrived
                 HIPCHK(hipSetDevice(s.device));
                 NCCLCHK(ncclAllReduce(s.d_count, s.d_count, 1, ncclUint64, ncclSum, s.comm, s.stream));
-                HIPCHK(hipStreamSynchronize(s.stream));
+                CHK(bounded_sync(s, "barrier all-reduce", -1));
             }
     return LIFE_OK;
 }
@@ -1059,21 +1115,31 @@ int stage_buffer(Shard &s, size_t bytes, uint8_t **out) {
 // kernel, 1 B per cell), VTK "%d\n" cell text (vtk kernel, 2 B per cell) or
 // BITS packed rows (bits kernel, LIFEBITS: bit x & 7 of byte x >> 3).  Every
 // shard exports its block on the device; in-process shards copy straight into
-// place, rank mode sends the blocks to the root (world-1) over RCCL.
-enum class Frame { DENSE, VTK, BITS };
+// place, rank mode sends the blocks to the root (world-1) over RCCL in the
+// order of life::gather_plan.
+enum class Frame { DENSE = life::kGatherDense, VTK = life::kGatherVtk, BITS = life::kGatherBits };
 
 int gather_impl(life_dev *d, uint8_t *out, Frame fmt) {
     const int root = d->world - 1;  // life_collect: cart rank of (dims0-1, dims1-1)
     const bool have_root = find_local(d, root) != nullptr;
     if (have_root && !out) return LIFE_EINVAL;
     CHK(life_dev_sync(d));
-    const int64_t frb = fmt == Frame::BITS ? (d->nx + 7) / 8 : d->nx * (fmt == Frame::VTK ? 2 : 1);  // frame row
-    auto row_bytes = [&](const life_layout &L) -> int64_t {
-        return fmt == Frame::BITS ? life::bits_row_bytes(L) : L.w * (fmt == Frame::VTK ? 2 : 1);
+    std::vector<life::GatherPiece> plan((size_t)d->world);
+    int64_t slot = 0;
+    if (life::gather_plan(d->nx, d->ny, d->dims[0], d->dims[1], d->kernel, (int)fmt, plan.data(), d->world,
+                          &slot) != d->world) {
+        set_err("gather plan failed");
+        return LIFE_EINVAL;
+    }
+    auto piece_of = [&](int rank) -> const life::GatherPiece & {
+        for (const life::GatherPiece &p : plan)
+            if (p.rank == rank) return p;
+        return plan[0];  // unreachable: every rank has a piece
     };
+    const int64_t frb = life::gather_frame_row_bytes(d->nx, (int)fmt);
     auto export_block = [&](Shard &s, uint8_t **stage) -> int {
         const life_layout &L = s.lay;
-        CHK(stage_buffer(s, (size_t)(row_bytes(L) * L.h), stage));
+        CHK(stage_buffer(s, (size_t)piece_of(s.rank).bytes, stage));
         if (fmt == Frame::DENSE)
             HIPCHK(life::launch_export_block(L, s.buf[s.cur], *stage, s.stream));
         else if (fmt == Frame::VTK)
@@ -1084,23 +1150,19 @@ int gather_impl(life_dev *d, uint8_t *out, Frame fmt) {
     };
     // BITS: a byte holding cells of two blocks (a block edge at x % 8 != 0)
     // is OR-ed together from both exports; those frame bytes start at 0
-    auto shared_first = [&](const life_layout &L) { return fmt == Frame::BITS && (L.x0 & 7) != 0; };
-    auto shared_last = [&](const life_layout &L) {
-        return fmt == Frame::BITS && ((L.x0 + L.w) & 7) != 0 && L.x0 + L.w < d->nx;
-    };
     std::vector<uint8_t> tmp;
-    auto place = [&](const life_layout &L, const uint8_t *src) -> int {
-        const int64_t rb = row_bytes(L);
-        uint8_t *dst = out + L.y0 * frb + (fmt == Frame::BITS ? (L.x0 >> 3) : L.x0 * (fmt == Frame::VTK ? 2 : 1));
-        if (!shared_first(L) && !shared_last(L)) {
+    auto place = [&](const life::GatherPiece &p, const uint8_t *src) -> int {
+        const int64_t rb = p.row_bytes;
+        uint8_t *dst = out + p.dst;
+        if (!p.shared_first && !p.shared_last) {
             // blocking: `out` is the caller's pageable memory
-            HIPCHK(hipMemcpy2D(dst, (size_t)frb, src, (size_t)rb, (size_t)rb, (size_t)L.h, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy2D(dst, (size_t)frb, src, (size_t)rb, (size_t)rb, (size_t)p.rows, hipMemcpyDeviceToHost));
             return LIFE_OK;
         }
-        tmp.resize((size_t)(rb * L.h));
+        tmp.resize((size_t)p.bytes);
         HIPCHK(hipMemcpy(tmp.data(), src, tmp.size(), hipMemcpyDeviceToHost));
-        const bool f = shared_first(L), l = shared_last(L);
-        for (int64_t y = 0; y < L.h; y++) {
+        const bool f = p.shared_first, l = p.shared_last;
+        for (int64_t y = 0; y < p.rows; y++) {
             uint8_t *o = dst + y * frb;
             const uint8_t *t = tmp.data() + y * rb;
             const int64_t a = f ? 1 : 0, b = l ? rb - 1 : rb;
@@ -1110,14 +1172,11 @@ int gather_impl(life_dev *d, uint8_t *out, Frame fmt) {
         }
         return LIFE_OK;
     };
-    if (fmt == Frame::BITS) {
+    if (fmt == Frame::BITS && have_root) {
         // zero the shared bytes of every block boundary (all ranks' blocks)
-        for (int r = 0; r < d->world && have_root; r++) {
-            life_layout L;
-            CHK(life_layout_query(d->nx, d->ny, d->dims[0], d->dims[1], r, d->kernel, &L));
-            if (shared_first(L))
-                for (int64_t y = 0; y < L.h; y++) out[(L.y0 + y) * frb + (L.x0 >> 3)] = 0;
-        }
+        for (const life::GatherPiece &p : plan)
+            if (p.shared_first)
+                for (int64_t y = 0; y < p.rows; y++) out[p.dst + y * frb] = 0;
     }
     if (!d->rank_mode) {
         for (Shard &s : d->shards) {
@@ -1128,7 +1187,7 @@ int gather_impl(life_dev *d, uint8_t *out, Frame fmt) {
         for (Shard &s : d->shards) {  // every export is queued before the first copy waits
             HIPCHK(hipSetDevice(s.device));
             HIPCHK(hipStreamSynchronize(s.stream));
-            CHK(place(s.lay, s.stage));
+            CHK(place(piece_of(s.rank), s.stage));
         }
         return LIFE_OK;
     }
@@ -1137,45 +1196,35 @@ int gather_impl(life_dev *d, uint8_t *out, Frame fmt) {
     uint8_t *stage;
     CHK(export_block(s, &stage));
     if (s.rank != root) {
-        NCCLCHK(ncclSend(stage, (size_t)(row_bytes(s.lay) * s.lay.h), ncclUint8, root, s.comm, s.stream));
-        HIPCHK(hipStreamSynchronize(s.stream));
-        return LIFE_OK;
+        if (!s.comm) {
+            set_err("gather: rank %d has no communicator", s.rank);
+            return LIFE_ESTATE;
+        }
+        NCCLCHK(ncclSend(stage, (size_t)piece_of(s.rank).bytes, ncclUint8, root, s.comm, s.stream));
+        return bounded_sync(s, "gather: send to the root", root);
     }
     HIPCHK(hipStreamSynchronize(s.stream));
-    int64_t maxb = 0;
-    for (int r = 0; r < d->world; r++) {
-        life_layout L;
-        CHK(life_layout_query(d->nx, d->ny, d->dims[0], d->dims[1], r, d->kernel, &L));
-        if (row_bytes(L) * L.h > maxb) maxb = row_bytes(L) * L.h;
-    }
     // The root's own block sits in the front of the staging buffer; two
     // receive slots follow.  Block k+1 arrives over RCCL (non-blocking
     // stream) while the host copies block k out of the other slot (a
     // blocking copy into the caller's pageable memory), so the fan-in of
     // world-1 blocks is not serialised behind the D2H copies.
-    const size_t slot = (size_t)maxb;
-    {
-        // grow keeping the exported block: copy it to the host first
-        CHK(place(s.lay, stage));
-        CHK(stage_buffer(s, 2 * slot, &stage));
+    CHK(place(plan[0], stage));  // copied out first: the buffer may grow below
+    CHK(stage_buffer(s, 2 * (size_t)slot, &stage));
+    if (d->world > 1 && !s.comm) {
+        set_err("gather: the root has no communicator");
+        return LIFE_ESTATE;
     }
-    std::vector<int> peers;
-    for (int r = 0; r < d->world; r++)
-        if (r != root) peers.push_back(r);
-    auto layout_of = [&](int r, life_layout *L) { return life_layout_query(d->nx, d->ny, d->dims[0], d->dims[1], r,
-                                                                           d->kernel, L); };
-    for (size_t k = 0; k < peers.size(); k++) {
-        life_layout L;
-        CHK(layout_of(peers[k], &L));
-        if (k == 0) NCCLCHK(ncclRecv(stage, (size_t)(row_bytes(L) * L.h), ncclUint8, peers[0], s.comm, s.stream));
-        HIPCHK(hipStreamSynchronize(s.stream));  // block k is in slot k % 2
-        if (k + 1 < peers.size()) {
-            life_layout Ln;
-            CHK(layout_of(peers[k + 1], &Ln));
-            NCCLCHK(ncclRecv(stage + ((k + 1) % 2) * slot, (size_t)(row_bytes(Ln) * Ln.h), ncclUint8, peers[k + 1],
-                             s.comm, s.stream));
+    for (size_t k = 1; k < plan.size(); k++) {
+        const life::GatherPiece &p = plan[k];
+        if (k == 1) NCCLCHK(ncclRecv(stage, (size_t)p.bytes, ncclUint8, p.rank, s.comm, s.stream));
+        CHK(bounded_sync(s, "gather: receive at the root", p.rank));  // block k is in slot p.slot
+        if (k + 1 < plan.size()) {
+            const life::GatherPiece &q = plan[k + 1];
+            NCCLCHK(ncclRecv(stage + (size_t)q.slot * (size_t)slot, (size_t)q.bytes, ncclUint8, q.rank, s.comm,
+                             s.stream));
         }
-        CHK(place(L, stage + (k % 2) * slot));
+        CHK(place(p, stage + (size_t)p.slot * (size_t)slot));
     }
     HIPCHK(hipStreamSynchronize(s.stream));
     return LIFE_OK;
@@ -1208,7 +1257,7 @@ static int census(life_dev *d, unsigned long long out[2]) {
         if (d->rank_mode && s.comm)
             NCCLCHK(ncclAllReduce(s.d_count, s.d_count, 2, ncclUint64, ncclSum, s.comm, s.stream));
         HIPCHK(hipMemcpyAsync(s.h_count, s.d_count, 2 * sizeof *s.h_count, hipMemcpyDeviceToHost, s.stream));
-        HIPCHK(hipStreamSynchronize(s.stream));  // pinned destination
+        CHK(bounded_sync(s, "census all-reduce", -1));  // pinned destination
         out[0] += s.h_count[0];
         out[1] += s.h_count[1];
     }
@@ -1279,6 +1328,10 @@ int life_dev_configure(life_dev *d, int option, int value) {
         d->flow = value & 3;
         d->flow_byte = (value & 4) != 0;
         return LIFE_OK;
+    case LIFE_OPT_FLOW_CHUNK:
+        if (value < 0) return LIFE_EINVAL;
+        d->flow_chunk = value;
+        return LIFE_OK;
     case LIFE_OPT_LOOPBACK: {
         if (value < 0 || value > 1) return LIFE_EINVAL;
         if (d->world != 1 || d->shards.size() != 1) {
@@ -1292,7 +1345,8 @@ int life_dev_configure(life_dev *d, int option, int value) {
             return LIFE_EINVAL;
         }
         if (value && d->transport == LIFE_XPORT_RCCL && !s.comm) {
-            set_err("loopback over RCCL needs a communicator (life_dev_create_rank with a unique id)");
+            set_err("loopback over RCCL needs a communicator (life_dev_create_rank with a unique id, or "
+                    "life_dev_create_ex with LIFE_XPORT_RCCL)");
             return LIFE_EINVAL;
         }
         // the current state's aprons are refreshed on the next step's first

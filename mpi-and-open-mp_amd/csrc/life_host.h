@@ -1,0 +1,49 @@
+// life_host.h -- host-only planning helpers of the runtime (life_plan.cpp):
+// no HIP types, so CPU tests compile life_plan.cpp with g++ alone and check
+// them without a GPU (tests/test_host_plan.py).
+#pragma once
+#include <stdint.h>
+
+#include "life_mi355x.h"
+
+namespace life {
+
+// life_halo_plan with `loop`: an axis with dims == 1 is exchanged too, the
+// shard being its own neighbour (LIFE_OPT_LOOPBACK).
+int halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int kernel, bool loop, life_halo_op *ops,
+              int max_ops);
+
+// The dataflow queue head is 32-bit: one launch may hold at most
+// kFlowMaxHead pulls (its items plus one extra pull per resident workgroup).
+// flow_chunk_passes: passes of `tiles` items each one launch of `grid`
+// resident workgroups may take (at most `cap` when cap > 0); 0 when not even
+// one pass fits.  Host-only (life_plan.cpp).
+constexpr int64_t kFlowMaxHead = (int64_t)1 << 31;
+int64_t flow_chunk_passes(int64_t tiles, int64_t grid, int64_t cap);
+
+// life_collect's fan-in (life_cart.c:281-305, 5-gather/life_mpi.c:177-179)
+// as a plan: every rank exports its block in one of three frame formats
+// (DENSE 1 B per cell, VTK 2 B, BITS = LIFEBITS packed rows), the root (rank
+// world-1) places its own block first, then receives the others in rank order
+// into two alternating staging slots (block k+1 arrives while block k is copied
+// out).  Pure arithmetic on life_layout_query, shared by the device gather
+// (life_dev.hip gather_impl) and the CPU tests.
+enum GatherFormat { kGatherDense = 0, kGatherVtk = 1, kGatherBits = 2 };
+struct GatherPiece {
+    int32_t rank;         // the block's global rank
+    int32_t slot;         // staging slot at the root: -1 = its own export, else 0 / 1
+    int64_t bytes;        // message size = row_bytes * rows
+    int64_t row_bytes;    // bytes per exported row
+    int64_t rows;         // block rows
+    int64_t dst;          // byte offset of its first row in the frame
+    int32_t shared_first; // BITS: its first byte of every row is shared with the block on its left (OR-ed)
+    int32_t shared_last;  // BITS: its last byte of every row is shared with the block on its right
+};
+int64_t gather_frame_row_bytes(int64_t nx, int fmt);
+// Fills pieces[0 .. world) (the root's own first, then ranks 0 .. world-2 in
+// receive order); *slot_bytes = the largest piece (one staging slot).
+// Returns world, or LIFE_EINVAL.
+int gather_plan(int64_t nx, int64_t ny, int dims0, int dims1, int kernel, int fmt, GatherPiece *pieces, int max,
+                int64_t *slot_bytes);
+
+}  // namespace life

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "life_host.h"
 #include "life_mi355x.h"
 
 namespace life {
@@ -137,11 +138,6 @@ inline bool self_wrap_x(const life_layout &L, int dims0) {
     return L.xapron == 32 && dims0 == 1 && L.w % 32 != 0;
 }
 hipError_t launch_wrap_columns(const life_layout &L, uint8_t *buf, hipStream_t s);
-
-// life_halo_plan with `loop`: an axis with dims == 1 is exchanged too, the
-// shard being its own neighbour (life_plan.cpp; LIFE_OPT_LOOPBACK).
-int halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int kernel, bool loop, life_halo_op *ops,
-              int max_ops);
 
 // Dense w*h byte block (row pitch w) <-> padded encoded buffer.
 hipError_t launch_import_block(const life_layout &L, const uint8_t *dense, uint8_t *buf,

@@ -1295,7 +1295,8 @@ StepTuning step_tuning(bool bit) { return tunings().t[bit ? 1 : 0]; }
 
 int temporal_rows(bool bit) {
     const int nr = tunings().nr[bit ? 1 : 0];
-    return temporal_rows_ok(nr) ? nr : (bit ? 48 : 32);
+    (void)bit;
+    return temporal_rows_ok(nr) ? nr : 48;
 }
 
 
@@ -1608,7 +1609,6 @@ hipError_t launch_tflow(const life_layout &L, const uint8_t *in, uint8_t *out, i
     f.items = passes * g.ntx * g.nty;
     f.head = head;
     f.done = done;
-    if (f.items >= (int64_t)UINT32_MAX) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(head, 0, sizeof(unsigned int), s);  // the error word is the caller's
     if (e == hipSuccess) e = hipMemsetAsync(done, 0, sizeof(unsigned int) * (size_t)(g.ntx * g.nty), s);
     if (e != hipSuccess) return e;
@@ -1617,6 +1617,8 @@ hipError_t launch_tflow(const life_layout &L, const uint8_t *in, uint8_t *out, i
     if (n <= 0) n = flow_slots(L);
     if (n <= 0) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)std::min<int64_t>(f.items, n);
+    // every workgroup pulls one item past the last: the 32-bit head must not wrap
+    if (f.items + (int64_t)grid > kFlowMaxHead) return hipErrorInvalidValue;
     void *args[] = {&f};
     return hipLaunchKernel(fn, dim3(grid), dim3(64 * kStackWaves), args, 0, s);
 }

@@ -11,6 +11,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "life_host.h"
 #include "life_mi355x.h"
 
 namespace {
@@ -18,11 +19,6 @@ constexpr int64_t kXoff = 128;  // owned x = 0 starts 128 B into a padded row
 inline int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 inline int cart_rank(int c0, int c1, int dims1) { return c0 * dims1 + c1; }
 }  // namespace
-
-namespace life {
-int halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int kernel, bool loop, life_halo_op *ops,
-              int max_ops);
-}
 
 extern "C" {
 
@@ -135,6 +131,46 @@ int life_layout_query(int64_t nx, int64_t ny, int dims0, int dims1, int rank, in
 }
 
 }  // extern "C"
+
+int64_t life::flow_chunk_passes(int64_t tiles, int64_t grid, int64_t cap) {
+    if (tiles < 1 || grid < 0 || cap < 0) return 0;
+    // items = passes * tiles; pulls = items + grid (each workgroup's last pull
+    // finds the queue empty) must stay <= kFlowMaxHead
+    int64_t n = (kFlowMaxHead - grid) / tiles;
+    if (n < 0) n = 0;
+    return cap > 0 && cap < n ? cap : n;
+}
+
+int64_t life::gather_frame_row_bytes(int64_t nx, int fmt) {
+    return fmt == kGatherBits ? (nx + 7) / 8 : nx * (fmt == kGatherVtk ? 2 : 1);
+}
+
+int life::gather_plan(int64_t nx, int64_t ny, int dims0, int dims1, int kernel, int fmt, GatherPiece *pieces,
+                      int max, int64_t *slot_bytes) {
+    if (dims0 < 1 || dims1 < 1 || fmt < kGatherDense || fmt > kGatherBits || !pieces || !slot_bytes) return LIFE_EINVAL;
+    const int world = dims0 * dims1;
+    if (max < world) return LIFE_EINVAL;
+    const int root = world - 1;  // life_collect: cart rank of (dims0-1, dims1-1)
+    const int64_t frb = gather_frame_row_bytes(nx, fmt);
+    int64_t big = 0;
+    for (int k = 0; k < world; k++) {
+        const int r = k == 0 ? root : k - 1;  // the root's own block, then the fan-in order
+        life_layout L;
+        if (life_layout_query(nx, ny, dims0, dims1, r, kernel, &L) != LIFE_OK) return LIFE_EINVAL;
+        GatherPiece &p = pieces[k];
+        p.rank = r;
+        p.slot = k == 0 ? -1 : (k - 1) % 2;
+        p.row_bytes = fmt == kGatherBits ? ((L.x0 & 7) + L.w + 7) / 8 : L.w * (fmt == kGatherVtk ? 2 : 1);
+        p.rows = L.h;
+        p.bytes = p.row_bytes * p.rows;
+        p.dst = L.y0 * frb + (fmt == kGatherBits ? (L.x0 >> 3) : L.x0 * (fmt == kGatherVtk ? 2 : 1));
+        p.shared_first = fmt == kGatherBits && (L.x0 & 7) != 0;
+        p.shared_last = fmt == kGatherBits && ((L.x0 + L.w) & 7) != 0 && L.x0 + L.w < nx;
+        if (p.bytes > big) big = p.bytes;
+    }
+    *slot_bytes = big;
+    return world;
+}
 
 // The halo plan; `loop` treats an axis the shard spans whole (dims == 1) as
 // partitioned too, with the shard as its own left and right neighbour

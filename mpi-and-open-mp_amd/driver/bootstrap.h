@@ -14,9 +14,11 @@
 int life_launcher_ranks(int *rank, int *world, int *local_rank);
 
 /* Rank 0 sends `id` to every other rank over TCP (LIFE_BOOTSTRAP_ADDR or
- * MASTER_ADDR, default 127.0.0.1; port LIFE_BOOTSTRAP_PORT, MASTER_PORT + 1,
- * or 29517); the others receive it, retrying the connection for up to
- * timeout_s seconds.  Returns 0 on success. */
+ * MASTER_ADDR -- an IPv4 address or a host name, resolved by getaddrinfo --
+ * default 127.0.0.1; port LIFE_BOOTSTRAP_PORT, MASTER_PORT + 1, or 29517);
+ * the others receive it, retrying the connection.  Every rank gives up after
+ * timeout_s seconds (rank 0 when a rank never connects).  Returns 0 on
+ * success, -1 on failure or timeout. */
 int life_bootstrap_id(int rank, int world, uint8_t id[LIFE_UID_BYTES], double timeout_s);
 
 #endif

@@ -114,6 +114,17 @@ void oracle_fill_random(int64_t nx, int64_t ny, uint64_t seed, uint32_t thr32, u
         }
 }
 
+void oracle_fill_random_window(int64_t nx, int64_t x0, int64_t y0, int64_t w, int64_t h, uint64_t seed,
+                               uint32_t thr32, uint8_t *out) {
+    const uint64_t key = oracle_splitmix64(seed);
+    for (int64_t y = 0; y < h; y++)
+        for (int64_t x = 0; x < w; x++) {
+            const int64_t gx = ((x0 + x) % nx + nx) % nx;
+            const uint64_t idx = (uint64_t)((y0 + y) * nx + gx);
+            out[y * w + x] = (uint32_t)(oracle_splitmix64(key ^ idx) >> 32) < thr32;
+        }
+}
+
 void oracle_decomposition(int64_t n, int p, int k, int64_t *start, int64_t *stop) {
     /* 6-cartesian/life_cart.c:217-223: equal blocks, the last takes the remainder. */
     const int64_t l = n / p;

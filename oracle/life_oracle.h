@@ -46,6 +46,11 @@ void oracle_life_run(int64_t nx, int64_t ny, uint8_t *grid, int64_t gens, int nt
  * cell(x,y) = (splitmix64(splitmix64(seed) ^ (y*nx + x)) >> 32) < thr32. */
 uint64_t oracle_splitmix64(uint64_t v);
 void oracle_fill_random(int64_t nx, int64_t ny, uint64_t seed, uint32_t thr32, uint8_t *grid);
+/* The same generator on a w x h window of a global nx-wide grid whose
+ * top-left cell is (x0, y0); x wraps modulo nx (a band across the x = 0
+ * seam), y does not. */
+void oracle_fill_random_window(int64_t nx, int64_t x0, int64_t y0, int64_t w, int64_t h, uint64_t seed,
+                               uint32_t thr32, uint8_t *out);
 
 /* decomposition(): 6-cartesian/life_cart.c:217-223, 64-bit. */
 void oracle_decomposition(int64_t n, int p, int k, int64_t *start, int64_t *stop);

@@ -51,6 +51,8 @@ def lib():
         L.oracle_splitmix64.argtypes = [ctypes.c_uint64]
         L.oracle_splitmix64.restype = ctypes.c_uint64
         L.oracle_fill_random.argtypes = [_i64, _i64, ctypes.c_uint64, ctypes.c_uint32, _u8p]
+        L.oracle_fill_random_window.argtypes = [_i64, _i64, _i64, _i64, _i64, ctypes.c_uint64, ctypes.c_uint32,
+                                                _u8p]
         L.oracle_decomposition.argtypes = [_i64, ctypes.c_int, ctypes.c_int,
                                            ctypes.POINTER(_i64), ctypes.POINTER(_i64)]
         L.oracle_dims_create.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
@@ -108,6 +110,14 @@ def step_padded(padded: np.ndarray, w: int, h: int) -> np.ndarray:
 def fill_random(nx: int, ny: int, seed: int, density: float = 0.5) -> np.ndarray:
     g = np.empty((ny, nx), dtype=np.uint8)
     lib().oracle_fill_random(nx, ny, seed, density_to_thr(density), _p(g))
+    return g
+
+
+def fill_random_window(nx: int, x0: int, y0: int, w: int, h: int, seed: int, density: float = 0.5) -> np.ndarray:
+    """fill_random's cells of the w x h window at (x0, y0) of a global
+    nx-wide grid (x modulo nx: a band may straddle the x = 0 seam)."""
+    g = np.empty((h, w), dtype=np.uint8)
+    lib().oracle_fill_random_window(nx, x0, y0, w, h, seed, density_to_thr(density), _p(g))
     return g
 
 

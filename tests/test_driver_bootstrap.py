@@ -87,3 +87,28 @@ def test_master_port_plus_one(harness):
     outs = [p.communicate(timeout=60)[0] for p in procs]
     assert all(p.returncode == 0 for p in procs), outs
     assert outs[0].split(" id ")[1] == outs[1].split(" id ")[1]
+
+
+def test_master_addr_hostname(harness):
+    """torchrun --standalone exports a host NAME as MASTER_ADDR; "localhost"
+    resolves through getaddrinfo (inet_pton accepted only dotted
+    quads)."""
+    port = free_port()
+    procs = [subprocess.Popen([harness], env=clean_env(RANK=r, WORLD_SIZE=2, MASTER_ADDR="localhost",
+                                                         MASTER_PORT=port - 1), stdout=subprocess.PIPE, text=True)
+             for r in (1, 0)]
+    outs = [p.communicate(timeout=60)[0] for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs
+    assert outs[0].split(" id ")[1] == outs[1].split(" id ")[1]
+
+
+def test_rank0_times_out_when_a_rank_never_connects(harness):
+    """Rank 0 of a 2-rank job whose rank 1 never starts: the accept wait is
+    bounded by the timeout (20 s in the harness) and fails, not a hang."""
+    import time
+
+    t = time.monotonic()
+    r = subprocess.run([harness], env=clean_env(RANK=0, WORLD_SIZE=2, LIFE_BOOTSTRAP_PORT=free_port()),
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and " rc -1 " in r.stdout, r.stdout
+    assert 15 < time.monotonic() - t < 45

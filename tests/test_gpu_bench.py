@@ -38,12 +38,14 @@ def test_strong_scaling_4_shards_full_size(kernel):
 
 
 @pytest.mark.parametrize("args", [("--gpus", "2", "--size", "8192", "--steps", "45", "--warmup", "4"),
+                                  ("--gpus", "2", "--size", "8192", "--partition", "rows", "--steps", "45",
+                                   "--warmup", "4"),
                                   ("--gpus", "3", "--size", "4096", "--partition", "cols", "--steps", "33",
                                    "--warmup", "0"),
                                   ("--gpus", "8", "--scaling", "strong", "--size", "8192", "--steps", "20",
                                    "--warmup", "5", "--parity-seconds", "0")])
 def test_multi_shard_bench_parity(args):
-    """Weak scaling row strips / column strips, and strong 4x2 blocks whose
+    """Weak scaling 2-D (default) / row strips / column strips, and strong 4x2 blocks whose
     parity leg is a fresh 3K+1-generation run (--parity-seconds 0)."""
     out = run_bench(*args)
     p = out["parity_vs_1gpu"]
@@ -53,6 +55,18 @@ def test_multi_shard_bench_parity(args):
     else:
         assert p["same_run"] is True
     assert out["phases"]["blocks"] > 0
+
+
+def test_weak_scaling_default_is_cartesian_8():
+    """configs[4] at N = 8: the weak line's
+    default partition is life_cart's MPI_Dims_create {4, 2} -- a 262144 x
+    131072 global grid of 65536^2 blocks, four halo peers per block -- and it
+    proves itself against the same grid run as one shard."""
+    out = run_bench("--gpus", "8", "--scaling", "weak", "--steps", "40", "--warmup", "8")
+    assert out["scaling"] == "weak" and out["config"]["dims"] == [4, 2]
+    assert (out["config"]["nx"], out["config"]["ny"]) == (262144, 131072)
+    assert out["config"]["partition"] == "cart"
+    assert out["parity_vs_1gpu"]["ok"] is True, out["parity_vs_1gpu"]
 
 
 def test_single_gpu_line_is_valu_roofline():

@@ -59,10 +59,35 @@ def test_flow_fullsize_census(gpu, n, m, flow):
         assert (life.checksum(), life.live_count()) == want
 
 
+def test_flow_back_to_back_and_chunked(gpu, oracle):
+    """Consecutive dataflow calls on one device: odd then even
+    pass counts (buffer parity flips between calls), a changed pass size
+    (the scratch is reused or regrown), and a call split over several
+    persistent launches (LIFE_OPT_FLOW_CHUNK: the 32-bit queue head's
+    chunking, forced small) -- each stage bit-exact against the oracle."""
+    nx, ny = 2048, 1000
+    g = oracle.fill_random(nx, ny, seed=31, density=0.45)
+    with gpu.Life(nx, ny, kernel="bit", small_grid=False) as life:
+        life.upload(g)
+        for gens, m, chunk in [(47, 20, 0), (61, 20, 0), (50, 12, 0), (89, 12, 3), (100, 20, 1), (41, 10, 2)]:
+            life.configure(gpu.OPT_BLOCK_GENS, m)
+            life.configure(gpu.OPT_FLOW_CHUNK, chunk)
+            life.set_timing(True)
+            life.step(gens)
+            assert life.last_path() == "flow"
+            if chunk:
+                _, launches, _ = life.kernel_stats()
+                assert launches >= gens // m  # timed per pass, however the passes were chunked
+            g = oracle.life_run(g, gens)
+            np.testing.assert_array_equal(life.gather(), g, err_msg=f"{gens} generations, m={m}, chunk={chunk}")
+
+
 def test_flow_rejected_options(gpu):
     with gpu.Life(256, 256, kernel="bit") as life:
         with pytest.raises(RuntimeError):
             life.configure(gpu.OPT_FLOW, 3)
+        with pytest.raises(RuntimeError):
+            life.configure(gpu.OPT_FLOW_CHUNK, -1)
 
 
 # byte encoding (LIFE_OPT_FLOW value | 4: opt-in): 16-B sc1 buffer loads /

@@ -23,12 +23,14 @@ CASES = [(256, 130, 45), (257, 131, 37), (512, 300, 70), (300, 64, 33), (31, 100
 
 
 def _make(gpu, nx, ny, kernel, rccl):
-    if rccl:
+    if rccl == "rank":  # one-process-per-GPU set-up: ncclCommInitRank at world 1
         return gpu.Life.for_rank(nx, ny, 0, 1, gpu.unique_id(), 0, kernel=kernel)
+    if rccl == "initall":  # single-process multi-device set-up: ncclCommInitAll over one device
+        return gpu.Life(nx, ny, kernel=kernel, transport=gpu.XPORT_RCCL)
     return gpu.Life(nx, ny, kernel=kernel)
 
 
-@pytest.mark.parametrize("rccl", [False, True], ids=["local", "rccl"])
+@pytest.mark.parametrize("rccl", [None, "rank", "initall"], ids=["local", "rccl", "rccl_initall"])
 @pytest.mark.parametrize("kernel", ["bit", "byte"])
 @pytest.mark.parametrize("nx,ny,gens", CASES)
 def test_loopback_parity(gpu, oracle, nx, ny, gens, kernel, rccl):
@@ -72,9 +74,11 @@ def test_loopback_rejected_for_partitioned(gpu):
 
 
 @pytest.mark.parametrize("kernel", ["bit", "byte"])
-def test_loopback_rccl_8192(gpu, kernel):
+@pytest.mark.parametrize("rccl", ["rank", "initall"])
+def test_loopback_rccl_8192(gpu, kernel, rccl):
     """8192^2 over RCCL loopback == the wrapped single shard (census checksum
-    and live count after several halo periods and a partial one)."""
+    and live count after several halo periods and a partial one), through
+    either communicator set-up."""
     n = 8192
     with gpu.Life(n, n, kernel=kernel) as ref:
         ref.fill_random(9, 0.5)
@@ -82,8 +86,32 @@ def test_loopback_rccl_8192(gpu, kernel):
         gens = 3 * K + 5
         ref.step(gens)
         want = (ref.checksum(), ref.live_count())
-    with gpu.Life.for_rank(n, n, 0, 1, gpu.unique_id(), 0, kernel=kernel) as life:
+    with _make(gpu, n, n, kernel, rccl) as life:
         life.fill_random(9, 0.5)
         life.configure(gpu.OPT_LOOPBACK, 1)
         life.step(gens)
         assert (life.checksum(), life.live_count()) == want
+
+
+def test_initall_world(gpu):
+    """The single-process RCCL device reports its transport (what bench.py
+    --gpus N takes with N real devices)."""
+    with gpu.Life(256, 256, kernel="bit", transport=gpu.XPORT_RCCL) as life:
+        w = life.world()
+        assert (w["world"], w["nlocal"], w["transport"]) == (1, 1, gpu.XPORT_RCCL)
+
+
+@pytest.mark.parametrize("kernel", ["bit", "byte"])
+def test_loopback_initall_gather_and_frames(gpu, oracle, kernel):
+    """Gather, VTK and LIFEBITS frames of an RCCL-loopback device after a
+    partial halo period equal the oracle's."""
+    nx, ny, gens = 640, 96, 45
+    g0 = oracle.fill_random(nx, ny, seed=5, density=0.5)
+    want = oracle.life_run(g0, gens)
+    with gpu.Life(nx, ny, kernel=kernel, transport=gpu.XPORT_RCCL) as life:
+        life.upload(g0)
+        life.configure(gpu.OPT_LOOPBACK, 1)
+        life.step(gens)
+        np.testing.assert_array_equal(life.gather(), want)
+        np.testing.assert_array_equal(life.gather_bits(), np.packbits(want, axis=1, bitorder="little"))
+        assert life.gather_vtk() == gpu.vtk_bytes(want)

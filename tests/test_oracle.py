@@ -127,3 +127,13 @@ def test_ref_mpirun_cfg_and_rate(oracle, lm, tmp_path):
         pytest.skip("oracle/_ref/life_cart or mpiexec not built here")
     r = ref_mpirun.steady_rate(oracle.fill_random(256, 256, 3, 0.5), 4, target_s=0.5, probe_gens=10)
     assert r["kind"] == "reference" and r["cores"] == 4 and r["value"] > 0
+
+
+def test_fill_random_window_matches_full_grid(oracle):
+    """The windowed generator (the 65536^2 band test's initial band) is the
+    full grid's cells, x taken modulo nx across the seam."""
+    nx, ny = 300, 40
+    g = oracle.fill_random(nx, ny, 7, 0.5)
+    w = oracle.fill_random_window(nx, -50, 3, 120, 20, 7, 0.5)
+    np.testing.assert_array_equal(w, np.roll(g, 50, axis=1)[3:23, :120])
+    np.testing.assert_array_equal(oracle.fill_random_window(nx, 0, 0, nx, ny, 7, 0.5), g)
