@@ -104,13 +104,17 @@ int life_halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int k
 
 /* Padded layout of a shard as allocated on the device: rows = h + 2*yapron
  * padded rows of `pitch` bytes; owned cell (x, y) lives in padded row
- * y + yapron at cell offset x from byte `xoff` (bit encoding: bit x&31 of the
- * little-endian dword (x>>5), floor division, counted from xoff).
- * `generations_per_exchange` is how many generations one halo exchange
- * feeds: 1 for the one-cell apron; for the temporally blocked stencil
- * (32-cell x-apron, K-row y-apron) K = LIFE_TEMPORAL_DEPTH (bit) or
- * LIFE_TEMPORAL_DEPTH_BYTE (byte), or 8/12/16/24/32 from the environment
- * variables of the same names. */
+ * y + yapron at cell offset x from byte `xoff`.  Byte encoding: byte x.  Bit
+ * encoding: 64-cell pairs of little-endian dwords, bit-interleaved -- cell x
+ * is bit ((x & 63) >> 1) of dword 2*(x >> 6) + (x & 1) (floor division,
+ * counted from xoff): the even cells of a pair in its first dword, the odd
+ * cells in its second (the stencil's horizontal neighbours then need one
+ * funnel shift per dword).  `generations_per_exchange` is how
+ * many generations one halo exchange feeds: 1 for the one-cell apron; for
+ * the temporally blocked stencil (x-apron of one lane column: 64 cells for
+ * bits, 32 for bytes; K-row y-apron; blocks at least that wide) K =
+ * LIFE_TEMPORAL_DEPTH (bit) or LIFE_TEMPORAL_DEPTH_BYTE (byte), or
+ * 8/12/16/24/32 from the environment variables of the same names. */
 #define LIFE_TEMPORAL_DEPTH 32
 #define LIFE_TEMPORAL_DEPTH_BYTE 32
 typedef struct {
@@ -262,13 +266,13 @@ int life_dev_set_timing(life_dev *d, int on);
 #define LIFE_OPT_LOOPBACK 6
 /* LIFE_OPT_FLOW (default 1, or LIFE_FLOW from the environment): a step call
  * on a single shard whose axes both wrap inside it (bit encoding, width a
- * multiple of 32) runs its whole passes of m generations (m = the block
+ * multiple of 64) runs its whole passes of m generations (m = the block
  * size, LIFE_OPT_BLOCK_GENS) as ONE persistent launch: workgroups pull
  * (pass, tile) items in order and a tile starts when the tiles its window
  * reads have finished the previous pass, so no pass boundary drains the chip;
  * the remainder runs as an ordinary launch.  1: write-through hand-off
- * stores; 2: plain stores + a release fence per tile; + 4: the byte
- * encoding too (default off, or LIFE_FLOW_BYTE=1).  Same results. */
+ * stores; 2: plain stores + a release fence per tile; 0: off.  The byte
+ * encoding always runs per-launch tiles.  Same results. */
 #define LIFE_OPT_FLOW 7
 /* LIFE_OPT_FLOW_CHUNK (default 0 = automatic): the dataflow launch's queue
  * head is a 32-bit counter, so a step call's passes are split over several
@@ -313,10 +317,13 @@ int life_dev_phase_stats(life_dev *d, double *ring_ms, double *interior_ms, doub
 int life_tune(int kernel, int rows, int depth);
 
 /* Temporal (generations_per_exchange = K > 1) tile height of encoding
- * `kernel` (-1: both): register rows per wave, 32/40/48/56/64/96; a tile is one
- * workgroup of 8 vertically stacked waves, 8*rows - 2K owned rows; 0 keeps
- * the current values (default 48 for both encodings, by measurement);
- * LIFE_TEMPORAL_ROWS / LIFE_TEMPORAL_ROWS_BYTE override at load time. */
+ * `kernel` (-1: both, each taking the value if valid for it): register rows
+ * per wave -- bit: 16/24/32 rows of 64-cell pairs (default 24), byte:
+ * 32/40/48/56/64/96 rows of 32-cell words (default 48); a tile is one
+ * workgroup of vertically stacked waves (8; bit: LIFE_TILE_WAVES 8/12/16 at
+ * load time for shapes with an instance), waves*rows - 2*ghost owned rows;
+ * 0 keeps the current values; LIFE_TEMPORAL_ROWS / LIFE_TEMPORAL_ROWS_BYTE
+ * override at load time. */
 int life_tune_temporal(int kernel, int rows);
 
 /* Measured HBM copy ceiling of `device` ("also report a

@@ -1,10 +1,22 @@
 // life_bitops.h -- bit-sliced Game-of-Life building blocks shared by the
-// gfx950 kernels (life_kernels.hip, life_sweep.hip).  Device code only.
+// gfx950 kernels (life_kernels.hip).  Device code only.
 //
-// One 32-cell word per lane, cell x at bit x.  A row's horizontal 3-sums are
-// a 2-bit number per cell (full adder of the cell and its two neighbours);
-// three rows' sums give n9 = u0 + 2*S, and the B3/S23 rule of
-// life_cart.c:202-208 / life2d.c:117-123 becomes 8 v_bitop3_b32.
+// BIT encoding layout (HBM and registers): cells come in 64-cell PAIRS of
+// dwords, bit-interleaved -- pair p of a row holds cells [64p, 64p + 64) as
+// E (dword 2p: bit i = cell 64p + 2i, the even cells) and O (dword 2p + 1:
+// bit i = cell 64p + 2i + 1, the odd cells).  The horizontal neighbours of an
+// even cell are the odd cells at the same bit of O and one bit below, of an
+// odd cell the even cells at the same bit of E and one bit above: a row's
+// 3-cell sums need ONE funnel shift per dword (v_alignbit, issued at half the
+// rate of v_bitop3 on gfx950: profiles/r01/ubench_valu.txt) instead of two
+// plus a DPP move for the natural layout -- 12.9 vs 16.4 ns per word and
+// generation in registers (profiles/r03/ubench_pair.txt).
+//
+// A row's horizontal 3-sums are a 2-bit number per cell (full adder of the
+// cell and its two neighbours); three rows' sums give n9 = u0 + 2*S, and the
+// B3/S23 rule of life_cart.c:202-208 / life2d.c:117-123 becomes 8
+// v_bitop3_b32 (a 3-gate tail is impossible: exhaustive search,
+// profiles/r03/rule_search.txt).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -25,11 +37,42 @@ constexpr uint32_t kEq2 = (~(0xF0 ^ 0xCC) & (0xAA ^ (0xF0 & 0xCC))) & 0xFF;  // 
 constexpr uint32_t kMux = ((0xF0 & 0xCC) | (~0xF0 & 0xAA)) & 0xFF;       // a ? b : c
 constexpr uint32_t kAndOr = (0xF0 & (0xCC | 0xAA)) & 0xFF;               // a & (b | c)
 
+// Pair layout of a cell x (x may be negative: aprons; arithmetic shifts give
+// floor division): dword index relative to the row's cell 0 and bit.
+__host__ __device__ __forceinline__ int64_t pair_dword(int64_t x) { return ((x >> 6) << 1) | (x & 1); }
+__host__ __device__ __forceinline__ uint32_t pair_bit(int64_t x) { return (uint32_t)((x & 63) >> 1); }
+
+// Bit (de)interleaving between a pair (E, O) and the natural 64-bit order
+// (bit j = cell j): helper kernels only (halo columns, frames, small grids).
+__device__ __forceinline__ uint32_t spread16(uint32_t x) {  // bit i -> bit 2i, i < 16
+    x &= 0xFFFFu;
+    x = (x | (x << 8)) & 0x00FF00FFu;
+    x = (x | (x << 4)) & 0x0F0F0F0Fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    return (x | (x << 1)) & 0x55555555u;
+}
+__device__ __forceinline__ uint32_t compact16(uint32_t x) {  // bit 2i -> bit i
+    x &= 0x55555555u;
+    x = (x | (x >> 1)) & 0x33333333u;
+    x = (x | (x >> 2)) & 0x0F0F0F0Fu;
+    x = (x | (x >> 4)) & 0x00FF00FFu;
+    return (x | (x >> 8)) & 0x0000FFFFu;
+}
+// 32 natural cells (bit k = cell k) from 16 even / 16 odd cells, and back
+__device__ __forceinline__ uint32_t nat32(uint32_t e16, uint32_t o16) { return spread16(e16) | (spread16(o16) << 1); }
+__device__ __forceinline__ uint64_t nat64(uint32_t e, uint32_t o) {
+    return (uint64_t)nat32(e, o) | ((uint64_t)nat32(e >> 16, o >> 16) << 32);
+}
+__device__ __forceinline__ uint2 pair_of(uint64_t v) {
+    const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    return make_uint2(compact16(lo) | (compact16(hi) << 16), compact16(lo >> 1) | (compact16(hi >> 1) << 16));
+}
+
 struct BitEnc {
-    static constexpr int64_t kCellsPerUnit = 128;
+    static constexpr int64_t kCellsPerUnit = 128;  // a 16-B unit = two pairs (E0, O0, E1, O1)
     static constexpr uint32_t kCell0 = 1u;
-    static __device__ __forceinline__ int64_t dword_of(int64_t x) { return x >> 5; }
-    static __device__ __forceinline__ uint32_t pos_in_dword(int64_t x) { return (uint32_t)(x & 31); }
+    static __device__ __forceinline__ int64_t dword_of(int64_t x) { return pair_dword(x); }
+    static __device__ __forceinline__ uint32_t pos_in_dword(int64_t x) { return pair_bit(x); }
     static __device__ __forceinline__ uint32_t top_shift(int64_t x) { return 31u - pos_in_dword(x); }
     struct H {
         uint32_t s0[4], s1[4];
@@ -40,12 +83,21 @@ struct BitEnc {
         s0 = b3<kXor3>(L, C, R);
         s1 = b3<kMaj>(L, C, R);
     }
+    // Horizontal sums of one pair: even cells 2i take O[i-1] + E[i] + O[i]
+    // (op: the O dword of the pair on the left, its bit 31 = cell 2i - 1 at
+    // i = 0), odd cells 2i+1 take E[i] + O[i] + E[i+1] (en: the E dword of
+    // the pair on the right, bit 0 = the cell after 2i + 1 at i = 31).
+    static __device__ __forceinline__ void pair_sums(uint32_t e, uint32_t o, uint32_t op, uint32_t en,
+                                                     uint32_t &e0, uint32_t &e1, uint32_t &o0, uint32_t &o1) {
+        fa(__builtin_amdgcn_alignbit(o, op, 31), e, o, e0, e1);
+        fa(e, o, __builtin_amdgcn_alignbit(en, e, 1), o0, o1);
+    }
+    // The 128 cells of a 16-B unit (two pairs); l: the O dword left of the
+    // unit, r: the E dword right of it.
     static __device__ __forceinline__ H hsum(uint4 d, uint32_t l, uint32_t r) {
         H h;
-        fa(__builtin_amdgcn_alignbit(d.x, l, 31), d.x, __builtin_amdgcn_alignbit(d.y, d.x, 1), h.s0[0], h.s1[0]);
-        fa(__builtin_amdgcn_alignbit(d.y, d.x, 31), d.y, __builtin_amdgcn_alignbit(d.z, d.y, 1), h.s0[1], h.s1[1]);
-        fa(__builtin_amdgcn_alignbit(d.z, d.y, 31), d.z, __builtin_amdgcn_alignbit(d.w, d.z, 1), h.s0[2], h.s1[2]);
-        fa(__builtin_amdgcn_alignbit(d.w, d.z, 31), d.w, __builtin_amdgcn_alignbit(r, d.w, 1), h.s0[3], h.s1[3]);
+        pair_sums(d.x, d.y, l, d.z, h.s0[0], h.s1[0], h.s0[1], h.s1[1]);
+        pair_sums(d.z, d.w, d.y, r, h.s0[2], h.s1[2], h.s0[3], h.s1[3]);
         return h;
     }
     // Rows a, b, c (2-bit horizontal sums) -> next state of the centre row.
@@ -74,7 +126,8 @@ __device__ __forceinline__ uint32_t bperm(int addr, uint32_t v) {
     return (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)v);
 }
 
-// Drifting frame: the next state of cell x-1 is computed at the bit that held
+// BYTE tiles (natural 32-cell words per lane, packed from bytes on load):
+// drifting frame: the next state of cell x-1 is computed at the bit that held
 // cell x, so a row's sums need only the LEFT neighbour word: with P the row's
 // bits, hsum at p = P[p-2] + P[p-1] + P[p] = LL + L + v (L = v << 1 | l >> 31,
 // LL = v << 2 | l >> 30, l by ds_bpermute), and the cell's own state is L.

@@ -127,10 +127,6 @@ static const int kEnvFlow = [] {
     const int v = e ? atoi(e) : 1;
     return v >= 0 && v <= 2 ? v : 1;
 }();
-static const bool kEnvFlowByte = [] {
-    const char *e = getenv("LIFE_FLOW_BYTE");
-    return e ? atoi(e) != 0 : false;
-}();
 static int default_block_gens(int kernel) {
     return kEnvBlockGens ? kEnvBlockGens : (kernel == LIFE_KERNEL_BIT ? 20 : 32);
 }
@@ -150,10 +146,9 @@ struct life_dev {
     int win_rows = 0, win_halo = 0;  // windowed kernel: strip height R, halo rows K (0: automatic)
     bool loop = false;  // LIFE_OPT_LOOPBACK: the one shard exchanges both axes' halos with itself
     int last_path = LIFE_PATH_NONE;  // life_dev_last_path
-    int flow = kEnvFlow;
-    bool flow_byte = kEnvFlowByte;
-    int64_t flow_chunk = 0;  // LIFE_OPT_FLOW_CHUNK: passes per dataflow launch at most (0: automatic)  // the dataflow form for the byte encoding too (LIFE_OPT_FLOW value | 4)  // LIFE_OPT_FLOW: single-shard bit tiles as one persistent dataflow launch per
+    int flow = kEnvFlow;  // LIFE_OPT_FLOW: single-shard bit tiles as one persistent dataflow launch per
                           // step call (1: write-through hand-off, 2: plain stores + release; 0 off)
+    int64_t flow_chunk = 0;  // LIFE_OPT_FLOW_CHUNK: passes per dataflow launch at most (0: automatic)
     std::vector<Shard> shards;
     double acc_ms = 0.0;
     int64_t acc_launches = 0;
@@ -481,7 +476,7 @@ int launch_tiles(life_dev *d, Shard &s, const life::TileRegion *r, int nreg, int
         HIPCHK(hipEventRecord(t->b, st));
         const life::TileGeom g = life::tile_geom(s.lay, m);
         for (int k = 0; k < nreg; k++) {
-            const int64_t xa = r[k].tx0 * g.words * 32, xb = std::min(r[k].tx1 * g.words * 32, s.lay.w);
+            const int64_t xa = r[k].tx0 * g.lanes * g.cells, xb = std::min(r[k].tx1 * g.lanes * g.cells, s.lay.w);
             const int64_t ya = r[k].ty0 * g.rows, yb = std::min(r[k].ty1 * g.rows, s.lay.h);
             if (xb > xa && yb > ya) {
                 // compulsory HBM bytes of the launch: each owned cell's bit is
@@ -557,10 +552,11 @@ int next_block(const life_dev *d, int64_t remaining) {
 // one K-deep halo exchange.  Partitioned shards: the boundary ring (one
 // multi-region launch) runs on the compute stream, the exchange of its new
 // state on the comm stream, and the interior concurrently on the second
-// compute stream.  The ring holds every tile / (strip, segment) that produces
-// a cell the exchange sends: rows [0, K) and [h-K, h), columns [0, 32) and
-// [w-32, w).  A self-wrapped x axis (life::self_wrap_x) counts as
-// partitioned: its "exchange" is the column copy.
+// compute stream.  The ring holds every tile that produces a cell the
+// exchange sends: rows [0, K) and [h-K, h), columns [0, xa) and [w-xa, w)
+// (xa = the x-apron, one lane column).  A self-wrapped x axis
+// (life::self_wrap_x) counts as partitioned: its "exchange" is the column
+// copy.
 int generation_block(life_dev *d, int m) {
     const bool rx = part(d, 0) || self_wrap_x(d), ry = part(d, 1);
     std::vector<PhaseEvents *> pe(d->shards.size(), nullptr);
@@ -573,9 +569,9 @@ int generation_block(life_dev *d, int m) {
         const life::TileGeom g = life::tile_geom(s.lay, m);
         const int64_t NX = g.ntx, NY = g.nty, uh = g.rows;
         int64_t ca = 0, cb = NX;
-        if (rx) {
+        if (rx) {  // the x-ring: tile columns holding cells [0, xa) and [w - xa, w)
             ca = 1;
-            cb = std::max(std::min(((s.lay.w - 32) / 32) / g.words, NX), ca);
+            cb = std::max(std::min(((s.lay.w - s.lay.xapron) / g.cells) / g.lanes, NX), ca);
         }
         auto launch = [&](const life::TileRegion *r, int n, bool timed, hipStream_t st) -> int {
             return launch_tiles(d, s, r, n, m, timed, st);
@@ -946,7 +942,7 @@ static int step_small(life_dev *d, int64_t generations) {
 static int step_flow(life_dev *d, int64_t generations, int64_t *done) {
     *done = 0;
     if (!d->flow || d->shards.size() != 1 || d->world != 1 || part(d, 0) || part(d, 1) ||
-        self_wrap_x(d) || (d->kernel == LIFE_KERNEL_BYTE && !d->flow_byte))
+        self_wrap_x(d) || d->kernel != LIFE_KERNEL_BIT)
         return LIFE_OK;
     Shard &s = d->shards[0];
     const life_layout &L = s.lay;
@@ -990,10 +986,9 @@ static int step_flow(life_dev *d, int64_t generations, int64_t *done) {
             HIPCHK(hipEventRecord(t->b, s.stream));
             t->launches = (int)n;  // stats: mean per pass
             const double cells = (double)L.w * (double)L.h;
-            const bool byte = d->kernel == LIFE_KERNEL_BYTE;
-            d->acc_bytes += (double)n * cells * (byte ? 2.0 : 0.25);
+            d->acc_bytes += (double)n * cells * 0.25;
             d->acc_updates += (double)n * cells * (double)m;
-            d->acc_valu += (double)n * (double)tiles * 64.0 * life::tstep_valu_per_tile_lane(m, byte);
+            d->acc_valu += (double)n * (double)tiles * 64.0 * life::tstep_valu_per_tile_lane(m, false);
         }
         if (n & 1) s.cur ^= 1;
         left -= n;
@@ -1324,9 +1319,8 @@ int life_dev_configure(life_dev *d, int option, int value) {
         d->block_gens = value > 0 ? value : default_block_gens(d->kernel);
         return LIFE_OK;
     case LIFE_OPT_FLOW:
-        if (value < 0 || (value & 3) > 2 || value > 6) return LIFE_EINVAL;
-        d->flow = value & 3;
-        d->flow_byte = (value & 4) != 0;
+        if (value < 0 || value > 2) return LIFE_EINVAL;
+        d->flow = value;
         return LIFE_OK;
     case LIFE_OPT_FLOW_CHUNK:
         if (value < 0) return LIFE_EINVAL;
@@ -1339,9 +1333,11 @@ int life_dev_configure(life_dev *d, int option, int value) {
             return LIFE_EINVAL;
         }
         Shard &s = d->shards[0];
-        // the apron a partitioned y axis needs: at least K rows to send
-        if (value && s.lay.h < s.lay.yapron) {
-            set_err("loopback: %lld rows < the %lld-row halo", (long long)s.lay.h, (long long)s.lay.yapron);
+        // the aprons a partitioned axis needs: at least K rows / one x-apron
+        // of columns to send
+        if (value && (s.lay.h < s.lay.yapron || s.lay.w < s.lay.xapron)) {
+            set_err("loopback: %lld x %lld cells < the %lld-column / %lld-row halo", (long long)s.lay.w,
+                    (long long)s.lay.h, (long long)s.lay.xapron, (long long)s.lay.yapron);
             return LIFE_EINVAL;
         }
         if (value && d->transport == LIFE_XPORT_RCCL && !s.comm) {
@@ -1419,8 +1415,11 @@ int life_tune(int kernel, int rows, int depth) {
 }
 
 int life_tune_temporal(int kernel, int rows) {
-    if ((rows && rows != 32 && rows != 40 && rows != 48 && rows != 56 && rows != 64 && rows != 96) || kernel < -1 ||
-        kernel > LIFE_KERNEL_BIT)
+    const bool bit_ok = rows == 16 || rows == 24 || rows == 32;
+    const bool byte_ok = rows == 32 || rows == 40 || rows == 48 || rows == 56 || rows == 64 || rows == 96;
+    if (kernel < -1 || kernel > LIFE_KERNEL_BIT) return LIFE_EINVAL;
+    if (rows && ((kernel == LIFE_KERNEL_BIT && !bit_ok) || (kernel == LIFE_KERNEL_BYTE && !byte_ok) ||
+                 (kernel == -1 && !bit_ok && !byte_ok)))
         return LIFE_EINVAL;
     life::set_temporal_rows(kernel, rows);
     return LIFE_OK;

@@ -48,16 +48,19 @@ StepTuning step_tuning(bool bit);
 void set_step_tuning(int kernel, int rows, int depth);  // kernel -1: both
 
 // Temporally blocked stencil (layouts with generations_per_exchange = K > 1,
-// either encoding): tiles of 62 32-cell word columns x `rows` rows (one
-// workgroup each), m <= min(K, 32) generations per launch from `in` to `out`;
-// a tile's window holds m ghost rows above and below, so the tile height
-// depends on m: tile_geom(L, m).
+// either encoding): tiles of 62 lane columns (bit: 64-cell interleaved pairs;
+// byte: 32-cell words) x `rows` rows (one workgroup each), m <= min(K, 32)
+// generations per launch from `in` to `out`; a bit tile's window holds m
+// ghost rows above and below (byte: K), so the tile height depends on m:
+// tile_geom(L, m).
 constexpr int kMaxRegions = 4;  // regions one temporal launch may hold
 struct TileRegion {
     int64_t tx0, tx1, ty0, ty1;
 };
 struct TileGeom {
-    int64_t words, rows, ntx, nty;
+    int64_t lanes;  // owned lane columns per tile (62)
+    int64_t cells;  // cells per lane column: 64 (bit pairs) or 32 (byte words)
+    int64_t rows, ntx, nty;
     int gsh;       // < 6: tile column bcol runs as bands of 2^gsh lanes (64 >> gsh tile rows per workgroup)
     int64_t bcol;  // the banded column (ntx - 1), -1 without banding
 };
@@ -67,8 +70,8 @@ TileGeom tile_geom(const life_layout &L, int m);
 int64_t region_items(const TileGeom &g, const TileRegion &r);
 int tile_ghost(const life_layout &L, int m);  // ghost rows per window end: m (bit) or K (byte)
 // Rows a temporally blocked buffer is allocated beyond its layout's `rows`:
-// the last tile's window (<= 8 waves x 96 rows) may read past the bottom
-// apron without clamping.
+// the last tile's window (<= 8 waves x 96 byte rows, 16 x 24 bit rows) may
+// read past the bottom apron without clamping.
 constexpr int64_t kTemporalSlackRows = 8 * 96;
 // Dataflow form of the tiles (tflow_kernel): `passes` launches of m
 // generations over a single shard whose axes both wrap inside it, as ONE
@@ -88,12 +91,13 @@ hipError_t launch_tflow(const life_layout &L, const uint8_t *in, uint8_t *out, i
 hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, const TileRegion *r, int nreg,
                         int m, Wrap wrap, hipStream_t s,
                         double *valu_lane_ops = nullptr);
-int temporal_rows(bool bit);      // register rows per wave (32/40/48/56/64/96)
+int temporal_rows(bool bit);      // register rows per wave: bit pair rows 16/24/32, byte word rows 32..96
+int tile_waves(bool bit);         // waves per tile workgroup: bit 8/12/16 (LIFE_TILE_WAVES), byte 8
 // VALU instructions the lanes at one lane position of a tile's waves issue
 // for m generations (the op-count model of life_kernels.hip tstep_kernel,
 // checked against the SQ_INSTS_VALU counter in profiles/); x 64 lanes x tiles.
 double tstep_valu_per_tile_lane(int m, bool byte);
-void set_temporal_rows(int kernel, int nr);  // kernel -1: both encodings
+void set_temporal_rows(int kernel, int nr);  // kernel -1: both encodings (values valid for each)
 
 // LDS-resident path for small single-shard grids: all `gens` generations in
 // one single-workgroup launch (in -> out; in may equal out).  Usable when
@@ -121,21 +125,23 @@ hipError_t launch_reg_win(const life_layout &L, const RegWinPlan &p, const uint8
 
 // Column halo staging: pack writes the last xapron columns to slot 0 and the
 // first xapron columns to slot 1 (h rows each: 1 byte 0/1 per row for a cell
-// column, the dword per row for a bit-encoded word column, 32 bytes per row
-// for a byte-encoded word column); unpack writes
-// slot 0 into x in [-xapron, 0) and slot 1 into [w, w + xapron).
+// column, one 8-B pair per row for a bit-encoded 64-cell column, 32 bytes per
+// row for a byte-encoded 32-cell column); unpack writes slot 0 into x in
+// [-xapron, 0) and slot 1 into [w, w + xapron).
 inline int64_t column_bytes_per_row(const life_layout &L) {
-    return L.xapron == 32 ? (L.kernel == LIFE_KERNEL_BIT ? 4 : 32) : 1;
+    if (L.xapron == 1) return 1;
+    return L.kernel == LIFE_KERNEL_BIT ? 8 : 32;
 }
 hipError_t launch_pack_columns(const life_layout &L, const uint8_t *buf, uint8_t *stage,
                                hipStream_t s);
 hipError_t launch_unpack_columns(const life_layout &L, uint8_t *buf, const uint8_t *stage,
                                  hipStream_t s);
 // Temporal layouts: a periodic x axis inside one shard is wrapped by the
-// stencil (whole words) when w % 32 == 0; otherwise the shard fills its own
-// 32-cell aprons from its own columns (launch_wrap_columns, needs w >= 32).
+// stencil (whole lane columns) when w is a multiple of the x-apron (64 bit
+// cells, 32 byte cells); otherwise the shard fills its own aprons from its own
+// columns (launch_wrap_columns, needs w >= xapron).
 inline bool self_wrap_x(const life_layout &L, int dims0) {
-    return L.xapron == 32 && dims0 == 1 && L.w % 32 != 0;
+    return L.xapron > 1 && dims0 == 1 && L.w % L.xapron != 0;
 }
 hipError_t launch_wrap_columns(const life_layout &L, uint8_t *buf, hipStream_t s);
 

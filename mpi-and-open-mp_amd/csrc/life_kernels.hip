@@ -243,146 +243,109 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs a) {
 // ------------------------------------------------------------------ temporal
 // Temporally blocked stencils (layouts with generations_per_exchange = K
 // > 1): m <= K generations per launch, each cell read once from and written
-// once to HBM per pass (plus the ghost rows of its window).  One tile body
-// (tile_body: an 8-wave workgroup per 62-word x (8R - 2m)-row tile, all m
-// generations of the tile in registers with one barrier per generation) in
-// two launch forms:
+// once to HBM per pass (plus the ghost rows of its window).  A tile is one
+// workgroup of NW vertically stacked waves holding a window of NW*R rows x 64
+// lane columns in registers, all m generations with one barrier each; lanes 0
+// and 63 are the tile's x-apron, so a tile owns 62 lane columns.  A lane
+// column is one interleaved pair (64 cells) for the bit encoding
+// (tile_body_bit) and one 32-cell word, packed from 32 byte cells on load,
+// for the byte encoding (tile_body_byte).  Two launch forms:
 //
 //  * tstep_kernel: one launch per pass, up to 4 tile regions (the boundary
 //    ring of a partitioned shard, or the whole shard);
-//  * tflow_kernel: every pass of a step call on a single wrapped shard in
-//    one persistent launch, tiles handed from pass to pass (LIFE_OPT_FLOW).
+//  * tflow_kernel (bit): every pass of a step call on a single wrapped shard
+//    in one persistent launch, tiles handed from pass to pass (LIFE_OPT_FLOW).
 
-constexpr int kStackWaves = 8;  // waves per tile workgroup (2 per SIMD; 12 measured slower, profiles/r02/r2w)
+constexpr int kStackWaves = 8;  // waves per byte tile workgroup (2 per SIMD; 12 measured slower, profiles/r02/r2w)
 struct TArgs {
     const uint8_t *in;
     uint8_t *out;
-    int64_t pitch, xoff, W, h, ya;  // W = 32-bit words per owned row
+    int64_t pitch, xoff, W, h, ya;  // W = lane columns per owned row: pairs (bit) or 32-cell words (byte)
     // up to kMaxRegions tile regions in one launch (the boundary ring of a
     // partitioned shard); workgroup b belongs to the region with first[k] <= b
     int64_t tx0[kMaxRegions], tx1[kMaxRegions], ty0[kMaxRegions], ty1[kMaxRegions], first[kMaxRegions + 1];
-    int32_t nreg, m;  // generations of the launch = ghost rows at each end of a window
+    int32_t nreg, m;  // generations of the launch = ghost rows at each end of a window (bit)
     // banded tile column (bit; tile_geom): gsh < 6 cuts the tiles of column
     // bcol into bands of G = 2^gsh lanes, 64 / G tile rows per workgroup; a
     // region whose tx1 == bcol + 1 lists its full tiles first, then its
     // ceil((ty1 - ty0) / (64 / G)) banded items
     int32_t gsh;
     int64_t bcol;
-    // tail split (R = 48, one launch of one full-width region): workgroups
-    // >= half_first run half-height tiles (R / 2 rows per wave) over rows
+    // tail split (bit, one launch of one full-width region): workgroups >=
+    // half_first run half-height tiles (R / 2 rows per wave) over rows
     // [half_y, half_yend), half_ntx per tile row, so the last round of a
     // launch is made of half-length items (launch_tstep)
     int64_t half_first, half_y, half_ntx, half_yend;
 };
 
-// Neighbour word from the left lane (DPP wave_shr:1, bound_ctrl: lane 0 reads
-// 0 -- its outer bits are allowed to be wrong).
-__device__ __forceinline__ uint32_t left_or_zero(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xf, 0xf, true);
-}
-// Centred-frame row sums (tstep, bit): the left word by DPP on the VALU, the
-// right one by ds_bpermute on the otherwise idle LDS pipe (+10 % over two DPP
-// moves, profiles/r01/hsum_modes.txt).  13 VALU + 1 LDS per row.
-__device__ __forceinline__ void bit_hsum(uint32_t v, uint32_t &s0, uint32_t &s1) {
-    const int lane = (int)__lane_id();
-    const uint32_t r = bperm(((lane + 1) & 63) << 2, v);
-    const uint32_t l = left_or_zero(v);
-    const uint32_t L = __builtin_amdgcn_alignbit(v, l, 31);
-    const uint32_t R = __builtin_amdgcn_alignbit(r, v, 1);
-    BitEnc::fa(L, v, R, s0, s1);
-}
+template <int NW>
+using Xch = uint32_t[2][NW][4][64];  // byte tiles: [parity][wave][top s0/s1, bottom s0/s1][lane]
+// bit tiles: [parity][1 + wave][top e0 e1 o0 o1, bottom ...][lane]; slots 0
+// and NW + 1 stay zero (the dead rows beyond the window): no branch on the
+// wave index in the generation loop
+template <int NW>
+using XchP = uint32_t[2][NW + 2][8][64];
 
-
-// tstep_kernel: one workgroup owns a tile of 62 word columns x T owned rows.
-// Its kStackWaves waves are stacked vertically: wave i holds window rows
-// [i*R, (i+1)*R) of a (kStackWaves*R)-row window that starts K rows above the
-// tile (T = kStackWaves*R - 2m for a launch of m generations), one 32-cell
-// word per lane and register row
-// (lane l holds word column 62*tx + l - 1; lanes 0 and 63 are the one-word
-// x-apron of the tile).  Each generation a wave publishes the horizontal sums
-// of its first and last row in LDS, one barrier, and takes its neighbours'
-// (the only values that cross waves); the window's own top/bottom K rows and
-// the edge lanes absorb the wrong values that enter from outside (K rows / K
-// <= 32 bits after K generations), so rows [K, K+T) of lanes 1..62 are exact.
-// Bit: centred frame (bit_hsum); byte: drifting frame (bit_hsum_drift; +2 %
-// there, -1 % for bit: profiles/r01/drift_ab.jsonl).
+// Bit tiles over interleaved pairs.  Lane l of a tile holds pair column
+// 62 tx + l - 1 of R consecutive window rows as (E, O) register pairs; wave
+// i holds window rows [iR, (i+1)R) of a window that starts m rows above the
+// tile, T = NW*R - 2m owned rows per tile.  Per generation and row: the
+// neighbour dwords of the lanes on either side by two ds_bpermute (the LDS
+// pipe; measured 4 % faster than a DPP move for the left one,
+// profiles/r03/ubench_pair.txt), 2 v_alignbit, 2 full adders (4 v_bitop3) for
+// the even and odd cells' horizontal sums, and the rule (8 v_bitop3) per
+// dword: 22 VALU + 2 LDS per pair-row, 11 VALU per 32 cells (the natural
+// one-word layout: 13).  Each generation a wave publishes the sums of its
+// first and last row in LDS (8 dwords per lane), one barrier, and takes its
+// neighbours'; the window's top and bottom m rows and the edge lanes absorb
+// the wrong values that enter from outside (m rows / m <= 32 cells after m
+// generations), so rows [m, NW*R - m) of lanes 1..62 are exact and stored.
 //
 // FLOW (tflow_kernel): the window is loaded with agent-scope (`sc1`,
-// L1-bypassing) loads, and stored with `sc1` write-through stores (FLOW 1)
-// or plain stores (FLOW 2, the kernel releases them with a fence): the rows
-// are another workgroup's output of the same launch.  Bit: 4-B atomic-form
-// loads / stores; byte: 16-B buffer loads / stores with the sc1 bit, one
-// buffer resource per row (a 65536^2 byte shard exceeds a resource's 32-bit
-// range).
-template <int NW>
-using Xch = uint32_t[2][NW][4][64];  // [parity][wave][top s0/s1, bottom s0/s1][lane]
-
-constexpr int kSc1 = 16;                  // buffer cache policy: sc1 (gfx94x/gfx950 CPol::SC1)
-constexpr int kRsrcFlags = 0x00020000;    // buffer resource dword 3 (gfx9 raw buffer, 32-bit data format)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const uint8_t *row, int64_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(row), 0, (int)bytes, kRsrcFlags);
-}
-__device__ __forceinline__ uint4 load16_sc1(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
-    const auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, kSc1);
-    return make_uint4(t[0], t[1], t[2], t[3]);
-}
-__device__ __forceinline__ void store16_sc1(__amdgpu_buffer_rsrc_t rs, uint32_t off, uint4 v) {
-    using V4 = unsigned int __attribute__((ext_vector_type(4)));
-    const V4 t = {v.x, v.y, v.z, v.w};
-    __builtin_amdgcn_raw_buffer_store_b128(t, rs, (int)off, 0, kSc1);
-}
-
-// Banded tiles (bit): a tile column that owns o <= 30 words (the last one:
-// W = 62 (ntx - 1) + o) wastes most of a 64-lane tile.  With gsh < 6 the wave
-// is cut into groups of G = 2^gsh lanes (1 ghost + o owned + ghost words),
-// group g holding tile row ty + g of that column: one workgroup carries nb <=
-// 64 / G tile rows ("bands").  The neighbour words a group's edge lanes fetch
+// L1-bypassing) 8-B atomic-form loads, and stored with `sc1` write-through
+// stores (FLOW 1) or plain stores (FLOW 2, the kernel releases them with a
+// fence): the rows are another workgroup's output of the same launch.
+//
+// Banded tiles: a tile column that owns o <= 30 pairs (the last one: W =
+// 62 (ntx - 1) + o) wastes most of a 64-lane tile.  With gsh < 6 the wave is
+// cut into groups of G = 2^gsh lanes (1 ghost + o owned + ghost pairs), group
+// g holding tile row ty + g of that column: one workgroup carries nb <= 64 /
+// G tile rows ("bands").  The neighbour dwords a group's edge lanes fetch
 // come from the adjacent group: garbage, exactly as a tile's lanes 0 / 63
-// read beyond the tile, absorbed by the ghost lanes (<= m <= 31 bits).  Only
-// the loads and stores differ (per-lane rows); the generation loop is the
-// tile's.  gsh = 6: an ordinary tile (nb = 1).
-template <bool BYTE, int R, int GK, bool WRAPX, bool WRAPY, int FLOW, int NW, bool BAND = false>
-__device__ __forceinline__ void tile_body(const TArgs &a, const uint8_t *in, uint8_t *out, int64_t tx, int64_t ty,
-                                          Xch<NW> &xch, int gsh = 6, int nb = 1, int64_t ybase = 0,
-                                          int64_t yend = -1) {
-    static_assert(R >= 3 && GK >= 0 && GK <= 32, "window");
-    // the window's ghost rows at each end: GK, or (GK = 0) the launch's
-    // generations m <= 32 (checked on the host); after m generations rows
-    // [ghost, NW*R - ghost) are exact.  The byte tiles keep a compile-time
-    // ghost depth: with a runtime one they ran 29 % slower (profiles/r02/
-    // ghost_ab.txt); the bit tiles run the same either way.
-    const int K = GK > 0 ? GK : a.m;
+// read beyond the tile, absorbed by the ghost lanes.  Only the loads and
+// stores differ (per-lane rows); the generation loop is the tile's.  gsh = 6:
+// an ordinary tile (nb = 1).
+template <int R, bool WRAPX, bool WRAPY, int FLOW, int NW, bool BAND = false>
+__device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in, uint8_t *out, int64_t tx,
+                                              int64_t ty, XchP<NW> &xch, int gsh = 6, int nb = 1,
+                                              int64_t ybase = 0, int64_t yend = -1) {
+    static_assert(R >= 3, "window");
+    const int K = a.m;  // ghost rows per window end
     const int T = NW * R - 2 * K;
-    constexpr bool DRIFT = BYTE;
     const int lane = threadIdx.x & 63;
-    const int laddr = ((lane - 1) & 63) << 2;
+    const int laddr = ((lane - 1) & 63) << 2, raddr = ((lane + 1) & 63) << 2;
     // wave index: uniform, so every row address below is scalar (SALU) math
     const int wi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // a separate instance: a runtime switch in the one body cost the ordinary
-    // tiles 5-12 % (profiles/r02/r2w: w8_b0 vs r2v).  Bit only: a byte BAND
-    // instance in the byte tiles cost them 7 % (profiles/r02/r3c)
-    constexpr bool banded = BAND && !BYTE;
-    const int gl = banded ? lane >> gsh : 0;                  // this lane's band (tile row ty + gl)
-    const int pin = banded ? lane & ((1 << gsh) - 1) : lane;  // lane within its group
-    const int64_t j = tx * 62 + pin - 1;                      // word column of this lane
+    const int gl = BAND ? lane >> gsh : 0;                  // this lane's band (tile row ty + gl)
+    const int pin = BAND ? lane & ((1 << gsh) - 1) : lane;  // lane within its group
+    const int64_t j = tx * 62 + pin - 1;                    // pair column of this lane
     int64_t jl;
     if (WRAPX) {
         jl = j % a.W;
         if (jl < 0) jl += a.W;
     } else {
-        jl = j > a.W ? a.W : j;  // words -1 .. W hold cells/apron; beyond: clamp (never stored)
+        jl = j > a.W ? a.W : j;  // pairs -1 .. W hold cells / apron; beyond: clamp (never stored)
     }
-    const uint32_t voff = (uint32_t)(a.xoff + (BYTE ? 32 : 4) * jl);
+    const uint32_t voff = (uint32_t)(a.xoff + 8 * jl);
     const int64_t y0 = ybase + ty * T - K + (int64_t)wi * R;  // owned row of register row 0 (>= -K)
     // Row pointers are walked: with a periodic y axis the walk wraps at h;
     // with an apron the last tile's window may run past the apron row h+K-1
     // into the allocation slack below the buffer (kTemporalSlackRows; those
     // rows are never stored).
     const uint8_t *row0 = in + a.ya * a.pitch;  // owned row 0
-    uint32_t v[R];
-    if (banded) {
-        // per-lane rows: band gl (lanes of bands >= nb load band nb - 1 and store nothing)
-        int64_t y = y0 + (int64_t)(gl < nb ? gl : nb - 1) * T;
+    uint32_t ve[R], vo[R];
+    {
+        int64_t y = y0 + (BAND ? (int64_t)(gl < nb ? gl : nb - 1) * T : 0);  // bands: per-lane rows
         if (WRAPY) {
             y %= a.h;
             if (y < 0) y += a.h;
@@ -390,9 +353,14 @@ __device__ __forceinline__ void tile_body(const TArgs &a, const uint8_t *in, uin
         const uint8_t *p = row0 + y * a.pitch;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            v[r] = FLOW ? __hip_atomic_load(reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(p) + voff),
-                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                        : *reinterpret_cast<const uint32_t *>(p + voff);
+            uint64_t q;
+            if (FLOW)
+                q = __hip_atomic_load(reinterpret_cast<uint64_t *>(const_cast<uint8_t *>(p) + voff),
+                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+                q = *reinterpret_cast<const uint64_t *>(p + voff);
+            ve[r] = (uint32_t)q;
+            vo[r] = (uint32_t)(q >> 32);
             ++y;
             if (WRAPY && y == a.h) {
                 y = 0;
@@ -401,70 +369,158 @@ __device__ __forceinline__ void tile_body(const TArgs &a, const uint8_t *in, uin
                 p += a.pitch;
             }
         }
-    } else {
-    int64_t y = y0;
-    if (WRAPY) {
-        y %= a.h;
-        if (y < 0) y += a.h;
     }
-    const uint8_t *p = row0 + y * a.pitch;
-    // Byte write-through hand-off (FLOW): line-contiguous sc1 loads, as the
-    // stores below -- lane l loads bytes 16 l.. and 1024 + 16 l.. of the tile
-    // span and packs each to 16 cells; lane s takes its word's halves from
-    // lanes 2 (s % 32) and 2 (s % 32) + 1 (low / high halves of their packed
-    // pair for s < 32 / s >= 32: one v_perm).  Lanes whose word wraps
-    // (WRAPX: word -1 or >= W) load it directly.  Beyond the row the buffer
-    // resource reads zeros.
-    const uint32_t lbase = (uint32_t)(a.xoff + 32 * (tx * 62 - 1)) + 16u * (uint32_t)lane;
-    const int g0 = 2 * (lane & 31);
-    const uint32_t psel = lane < 32 ? 0x05040100u : 0x07060302u;
-    const bool wrapped = WRAPX && (j < 0 || j >= a.W);
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        if (BYTE && FLOW) {
-            const __amdgpu_buffer_rsrc_t rs = row_rsrc(p, a.pitch);
-            const uint32_t P = pack16(load16_sc1(rs, lbase)) | (pack16(load16_sc1(rs, lbase + 1024u)) << 16);
-            const uint32_t q0 = bperm(g0 << 2, P), q1 = bperm((g0 + 1) << 2, P);
-            uint32_t w = __builtin_amdgcn_perm(q1, q0, psel);
-            if (wrapped) w = pack32(load16_sc1(rs, voff), load16_sc1(rs, voff + 16));
-            v[r] = w;
-        } else if (BYTE) {
-            const uint4 *q = reinterpret_cast<const uint4 *>(p + voff);
-            v[r] = pack32(q[0], q[1]);
-        } else if (FLOW) {
-            v[r] = __hip_atomic_load(reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(p) + voff), __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            v[r] = *reinterpret_cast<const uint32_t *>(p + voff);
-        }
-        ++y;
-        if (WRAPY && y == a.h) {
-            y = 0;
-            p = row0;
-        } else {
-            p += a.pitch;
-        }
-    }
-    }
-    auto hsum = [&](uint32_t x, uint32_t &s0, uint32_t &s1, uint32_t &L) {
-        if (DRIFT) {
-            bit_hsum_drift(x, laddr, s0, s1, L);
-        } else {
-            bit_hsum(x, s0, s1);
-            L = x;
-        }
+    auto hsum = [&](uint32_t e, uint32_t o, uint32_t &e0, uint32_t &e1, uint32_t &o0, uint32_t &o1) {
+        BitEnc::pair_sums(e, o, bperm(laddr, o), bperm(raddr, e), e0, e1, o0, o1);
     };
+    // Register budget (80 VGPRs at 3 tiles per CU, R = 24: 48 hold the
+    // window): only the rolling sums of three rows stay live across the
+    // loop.  Row 0 is updated first (its upper neighbour's sums come from LDS
+    // right after the barrier), the bottom row's own sums and the row below
+    // the wave are read back from LDS when row R-1 is reached.  No branch on
+    // the wave index inside the loop (the zero slots stand for the dead rows
+    // beyond the window): a branch there split the loop body into blocks and
+    // the every row's ds_bpermute was hoisted above it, their 2R results
+    // spilling (46-83 VGPRs at R = 24).
+    if (wi == 0 || wi == NW - 1)  // the dead slots (ordered by the first barrier below)
+        for (int q = 0; q < 16; ++q) xch[q >> 3][wi == 0 ? 0 : NW + 1][q & 7][lane] = 0u;
     for (int g = 0; g < a.m; ++g) {
         const int par = g & 1;
-        uint32_t t0, t1, b0, b1, tL, bL;  // xL: the row's own cells in the frame used
-        hsum(v[0], t0, t1, tL);
-        hsum(v[R - 1], b0, b1, bL);
+        uint32_t pe0, pe1, po0, po1, ce0, ce1, co0, co1;
+        {
+            uint32_t be0, be1, bo0, bo1;
+            hsum(ve[R - 1], vo[R - 1], be0, be1, bo0, bo1);
+            xch[par][wi + 1][4][lane] = be0;
+            xch[par][wi + 1][5][lane] = be1;
+            xch[par][wi + 1][6][lane] = bo0;
+            xch[par][wi + 1][7][lane] = bo1;
+        }
+        hsum(ve[0], vo[0], pe0, pe1, po0, po1);
+        xch[par][wi + 1][0][lane] = pe0;
+        xch[par][wi + 1][1][lane] = pe1;
+        xch[par][wi + 1][2][lane] = po0;
+        xch[par][wi + 1][3][lane] = po1;
+        __syncthreads();
+        hsum(ve[1], vo[1], ce0, ce1, co0, co1);
+        {
+            // the wave above (slot 0 above the window: zero, dead ghost rows)
+            const uint32_t ae0 = xch[par][wi][4][lane], ae1 = xch[par][wi][5][lane];
+            const uint32_t ao0 = xch[par][wi][6][lane], ao1 = xch[par][wi][7][lane];
+            ve[0] = BitEnc::rule1(ae0, ae1, pe0, pe1, ce0, ce1, ve[0]);
+            vo[0] = BitEnc::rule1(ao0, ao1, po0, po1, co0, co1, vo[0]);
+        }
+#pragma unroll
+        for (int r = 1; r < R - 1; ++r) {
+            uint32_t ne0, ne1, no0, no1;
+            if (r + 1 == R - 1) {  // published before the barrier
+                ne0 = xch[par][wi + 1][4][lane];
+                ne1 = xch[par][wi + 1][5][lane];
+                no0 = xch[par][wi + 1][6][lane];
+                no1 = xch[par][wi + 1][7][lane];
+            } else {
+                hsum(ve[r + 1], vo[r + 1], ne0, ne1, no0, no1);
+            }
+            ve[r] = BitEnc::rule1(pe0, pe1, ce0, ce1, ne0, ne1, ve[r]);
+            vo[r] = BitEnc::rule1(po0, po1, co0, co1, no0, no1, vo[r]);
+            pe0 = ce0;
+            pe1 = ce1;
+            po0 = co0;
+            po1 = co1;
+            ce0 = ne0;
+            ce1 = ne1;
+            co0 = no0;
+            co1 = no1;
+        }
+        {
+            // the wave below (slot NW + 1 below the window: zero)
+            const uint32_t de0 = xch[par][wi + 2][0][lane], de1 = xch[par][wi + 2][1][lane];
+            const uint32_t do0 = xch[par][wi + 2][2][lane], do1 = xch[par][wi + 2][3][lane];
+            ve[R - 1] = BitEnc::rule1(pe0, pe1, ce0, ce1, de0, de1, ve[R - 1]);
+            vo[R - 1] = BitEnc::rule1(po0, po1, co0, co1, do0, do1, vo[R - 1]);
+        }
+    }
+    // window rows [K, NW*R - K) are the tile's owned rows [ty*T, ty*T + T);
+    // this wave's share of them (a half-height tile's ghost rows may span more
+    // than one wave: K > R)
+    const int r0 = min(max(K - wi * R, 0), R), r1 = min(max(NW * R - K - wi * R, 0), R);
+    const bool st = BAND ? (pin >= 1 && pin <= (1 << gsh) - 2 && j < a.W && gl < nb)
+                         : (lane >= 1 && lane <= 62 && j < a.W);
+    const int64_t yb = y0 + (BAND ? (int64_t)(gl < nb ? gl : 0) * T : 0);  // this lane's band
+    const int64_t ylim = yend >= 0 ? yend : a.h;  // half tiles of a region stop at its last row
+    uint8_t *q = out + (a.ya + yb + r0) * a.pitch + voff;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (r < r0 || r >= r1) continue;
+        if (st && yb + r < ylim) {
+            const uint64_t v = (uint64_t)ve[r] | ((uint64_t)vo[r] << 32);
+            if (FLOW == 1)
+                __hip_atomic_store(reinterpret_cast<uint64_t *>(q), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+                *reinterpret_cast<uint64_t *>(q) = v;
+        }
+        q += a.pitch;
+    }
+}
+
+// Byte tiles: lane l of a tile holds word column 62 tx + l - 1 -- 32 byte
+// cells, packed into one register word per row by v_dot4_u32_u8 on load
+// (two 16-B loads) and unpacked on store -- in the drifting frame
+// (bit_hsum_drift: left neighbour only, 12 VALU + 1 LDS per row and
+// generation; +2 % over the centred frame for bytes,
+// profiles/r01/drift_ab.jsonl).  GK ghost rows per window end, compile-time
+// (a runtime depth measured 29 % slower here, profiles/r02/ghost_ab.txt).
+// The same window / exchange / barrier scheme as the bit tiles.
+template <int R, int GK, bool WRAPX, bool WRAPY, int NW>
+__device__ __forceinline__ void tile_body_byte(const TArgs &a, const uint8_t *in, uint8_t *out, int64_t tx,
+                                               int64_t ty, Xch<NW> &xch) {
+    static_assert(R >= 3 && GK >= 1 && GK <= 32, "window");
+    constexpr int K = GK;
+    constexpr int T = NW * R - 2 * K;
+    const int lane = threadIdx.x & 63;
+    const int laddr = ((lane - 1) & 63) << 2;
+    const int wi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t j = tx * 62 + lane - 1;  // word column of this lane
+    int64_t jl;
+    if (WRAPX) {
+        jl = j % a.W;
+        if (jl < 0) jl += a.W;
+    } else {
+        jl = j > a.W ? a.W : j;
+    }
+    const uint32_t voff = (uint32_t)(a.xoff + 32 * jl);
+    const int64_t y0 = ty * T - K + (int64_t)wi * R;
+    const uint8_t *row0 = in + a.ya * a.pitch;
+    uint32_t v[R];
+    {
+        int64_t y = y0;
+        if (WRAPY) {
+            y %= a.h;
+            if (y < 0) y += a.h;
+        }
+        const uint8_t *p = row0 + y * a.pitch;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint4 *q = reinterpret_cast<const uint4 *>(p + voff);
+            v[r] = pack32(q[0], q[1]);
+            ++y;
+            if (WRAPY && y == a.h) {
+                y = 0;
+                p = row0;
+            } else {
+                p += a.pitch;
+            }
+        }
+    }
+    for (int g = 0; g < a.m; ++g) {
+        const int par = g & 1;
+        uint32_t t0, t1, b0, b1, tL, bL;  // xL: the row's own cells in the drifting frame
+        bit_hsum_drift(v[0], laddr, t0, t1, tL);
+        bit_hsum_drift(v[R - 1], laddr, b0, b1, bL);
         xch[par][wi][0][lane] = t0;
         xch[par][wi][1][lane] = t1;
         xch[par][wi][2][lane] = b0;
         xch[par][wi][3][lane] = b1;
         __syncthreads();
-        // the row above the window / below it: dead (window ghost rows)
         uint32_t a0 = 0u, a1 = 0u, d0 = 0u, d1 = 0u;
         if (wi > 0) {
             a0 = xch[par][wi - 1][2][lane];
@@ -474,10 +530,8 @@ __device__ __forceinline__ void tile_body(const TArgs &a, const uint8_t *in, uin
             d0 = xch[par][wi + 1][0][lane];
             d1 = xch[par][wi + 1][1][lane];
         }
-        // rows 1 .. R-2 need only this wave's rows: they run while the LDS
-        // reads are in flight
         uint32_t p0 = t0, p1 = t1, c0, c1, cL;
-        hsum(v[1], c0, c1, cL);
+        bit_hsum_drift(v[1], laddr, c0, c1, cL);
         const uint32_t h10 = c0, h11 = c1;
 #pragma unroll
         for (int r = 1; r < R - 1; ++r) {
@@ -487,7 +541,7 @@ __device__ __forceinline__ void tile_body(const TArgs &a, const uint8_t *in, uin
                 n1 = b1;
                 nL = bL;
             } else {
-                hsum(v[r + 1], n0, n1, nL);
+                bit_hsum_drift(v[r + 1], laddr, n0, n1, nL);
             }
             v[r] = BitEnc::rule1(p0, p1, c0, c1, n0, n1, cL);
             cL = nL;
@@ -499,79 +553,36 @@ __device__ __forceinline__ void tile_body(const TArgs &a, const uint8_t *in, uin
         v[R - 1] = BitEnc::rule1(p0, p1, b0, b1, d0, d1, bL);
         v[0] = BitEnc::rule1(a0, a1, t0, t1, h10, h11, tL);
     }
-    // window rows [K, NW*R - K) are the tile's owned rows [ty*T, ty*T + T);
-    // this wave's share of them (a half-height tile's ghost rows may span more
-    // than one wave: K > R)
     const int r0 = min(max(K - wi * R, 0), R), r1 = min(max(NW * R - K - wi * R, 0), R);
-    if (banded) {
-        const int G = 1 << gsh;
-        const bool st = pin >= 1 && pin <= G - 2 && j < a.W && gl < nb;
-        const int64_t yb = y0 + (int64_t)(gl < nb ? gl : 0) * T;  // this lane's band
-        uint8_t *q = out + (a.ya + yb + r0) * a.pitch + voff;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            if (r < r0 || r >= r1) continue;
-            if (st && yb + r < a.h) {
-                if (FLOW == 1)
-                    __hip_atomic_store(reinterpret_cast<uint32_t *>(q), v[r], __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                else
-                    *reinterpret_cast<uint32_t *>(q) = v[r];
-            }
-            q += a.pitch;
-        }
-        return;
-    }
     const bool st = lane >= 1 && lane <= 62 && j < a.W;
-    const int64_t ylim = yend >= 0 ? yend : a.h;  // half tiles of a region stop at its last row
     uint8_t *q = out + (a.ya + y0 + r0) * a.pitch + voff;
-    // Byte write-through (FLOW 1) stores are not merged in L2, so each store
-    // instruction covers whole lines: lane l writes bytes [16 l, 16 l + 16) and
-    // [1024 + 16 l, ...) of the tile's 64-word span -- half (l & 1) of the
-    // words of lanes l >> 1 and 32 + (l >> 1), fetched by two ds_bpermute.
-    // (Lane-major 2 x 16 B per lane wrote every line twice: WRITE_SIZE 2x the
-    // per-launch tiles', profiles/r02/r3j.)
-    const int sa = lane >> 1, sb = 32 + (lane >> 1);  // source lanes
-    const bool st_a = sa >= 1 && sa <= 62 && tx * 62 + sa - 1 < a.W;
-    const bool st_b = sb >= 1 && sb <= 62 && tx * 62 + sb - 1 < a.W;
-    const uint32_t vbase = (uint32_t)(a.xoff + 32 * (tx * 62 - 1)) + 16u * (uint32_t)lane;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         if (r < r0 || r >= r1) continue;
-        if (DRIFT) v[r] = drift_realign(v[r], a.m);  // every lane: the bpermute reads lane + 1
-        if (BYTE && FLOW == 1) {
-            const uint32_t wa = bperm(sa << 2, v[r]), wb = bperm(sb << 2, v[r]);  // every lane
-            if (y0 + r < ylim) {
-                const __amdgpu_buffer_rsrc_t rs = row_rsrc(q - voff, a.pitch);  // the row: uniform
-                if (st_a) store16_sc1(rs, vbase, unpack_half(wa, lane & 1));
-                if (st_b) store16_sc1(rs, vbase + 1024u, unpack_half(wb, lane & 1));
-            }
-            q += a.pitch;
-            continue;
-        }
-        if (st && y0 + r < ylim) {
-            if (BYTE) {
-                uint4 *o = reinterpret_cast<uint4 *>(q);
-                o[0] = unpack_half(v[r], 0);
-                o[1] = unpack_half(v[r], 1);
-            } else if (FLOW == 1) {
-                __hip_atomic_store(reinterpret_cast<uint32_t *>(q), v[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-                *reinterpret_cast<uint32_t *>(q) = v[r];
-            }
+        v[r] = drift_realign(v[r], a.m);  // every lane: the bpermute reads lane + 1
+        if (st && y0 + r < a.h) {
+            uint4 *o = reinterpret_cast<uint4 *>(q);
+            o[0] = unpack_half(v[r], 0);
+            o[1] = unpack_half(v[r], 1);
         }
         q += a.pitch;
     }
 }
 
-template <bool BYTE, int R, int GK, bool WRAPX, bool WRAPY, int NW>
-__global__ __launch_bounds__(64 * NW, 4) void tstep_kernel(TArgs a) {
-    __shared__ Xch<NW> xch;
+// Waves per SIMD the bit tiles are compiled for (the VGPR budget): 3 tiles
+// of 8 waves or 2 of 12 per CU at <= 80 VGPRs; 16-wave tiles: 2 per CU at 64
+// (R = 16) or 1 at 128.
+constexpr int bit_wpe(int NW, int R) { return NW == 16 ? (R <= 16 ? 8 : 4) : (R <= 24 ? 6 : 4); }
+
+// One workgroup per tile (or banded item / half-height tail tile).
+template <int R, bool WRAPX, bool WRAPY, int NW>
+__global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tstep_bit_kernel(TArgs a) {
+    __shared__ XchP<NW> xch;
     const int64_t wg = blockIdx.x;
-    if (R == 48 && a.half_first > 0 && wg >= a.half_first) {
+    if (a.half_first > 0 && wg >= a.half_first) {
         const int64_t i = wg - a.half_first;
-        tile_body<BYTE, R / 2, GK, WRAPX, WRAPY, 0, NW>(a, a.in, a.out, i % a.half_ntx, i / a.half_ntx, xch, 6, 1,
-                                                        a.half_y, a.half_yend);
+        tile_body_bit<R / 2, WRAPX, WRAPY, 0, NW>(a, a.in, a.out, i % a.half_ntx, i / a.half_ntx, xch, 6, 1,
+                                                  a.half_y, a.half_yend);
         return;
     }
     const int64_t nwg = a.first[a.nreg];
@@ -584,12 +595,26 @@ __global__ __launch_bounds__(64 * NW, 4) void tstep_kernel(TArgs a) {
     const int64_t nfull = ntx * (a.ty1[k] - a.ty0[k]);
     if (wr < nfull) {
         const int64_t tx = a.tx0[k] + wr % ntx, ty = a.ty0[k] + wr / ntx;
-        tile_body<BYTE, R, GK, WRAPX, WRAPY, 0, NW>(a, a.in, a.out, tx, ty, xch);
-    } else if (!BYTE) {
+        tile_body_bit<R, WRAPX, WRAPY, 0, NW>(a, a.in, a.out, tx, ty, xch);
+    } else {
         const int64_t B = 64 >> a.gsh, ty = a.ty0[k] + (wr - nfull) * B;
         const int nb = (int)(a.ty1[k] - ty < B ? a.ty1[k] - ty : B);
-        tile_body<BYTE, R, GK, WRAPX, WRAPY, 0, NW, true>(a, a.in, a.out, a.bcol, ty, xch, a.gsh, nb);
+        tile_body_bit<R, WRAPX, WRAPY, 0, NW, true>(a, a.in, a.out, a.bcol, ty, xch, a.gsh, nb);
     }
+}
+
+template <int R, int GK, bool WRAPX, bool WRAPY, int NW>
+__global__ __launch_bounds__(64 * NW, 4) void tstep_byte_kernel(TArgs a) {
+    __shared__ Xch<NW> xch;
+    const int64_t wg = blockIdx.x;
+    const int64_t nwg = a.first[a.nreg];
+    if (wg >= nwg) return;
+    int k = 0;
+    while (k + 1 < a.nreg && wg >= a.first[k + 1]) ++k;
+    const int64_t wr = wg - a.first[k];
+    const int64_t ntx = a.tx1[k] - a.tx0[k];
+    const int64_t tx = a.tx0[k] + wr % ntx, ty = a.ty0[k] + wr / ntx;
+    tile_body_byte<R, GK, WRAPX, WRAPY, NW>(a, a.in, a.out, tx, ty, xch);
 }
 
 // tflow_kernel: `passes` launches of the bit tiles (m generations each, both
@@ -616,13 +641,12 @@ struct FArgs {
     unsigned int *done;              // per tile: passes completed (zeroed before the launch)
 };
 
-// bit: 3 tiles per CU (80 VGPRs); byte: 2 (its 92 VGPRs).  No banded column
-// here: the banded items in this loop cost the ordinary tiles 2.5 % (code
-// size in the persistent loop; profiles/r02/r2x: b0 / b1 vs base), more than
-// they save.
-template <bool BYTE, int R, int GK, bool WRAPX, bool WRAPY, int FLOW, int NW>
-__global__ __launch_bounds__(64 * NW, BYTE ? 4 : 6) void tflow_kernel(FArgs f) {
-    __shared__ Xch<NW> xch;
+// No banded column here: the banded items in this loop cost the ordinary
+// tiles 2.5 % (code size in the persistent loop; profiles/r02/r2x: b0 / b1 vs
+// base), more than they save.
+template <int R, bool WRAPX, bool WRAPY, int FLOW, int NW>
+__global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tflow_kernel(FArgs f) {
+    __shared__ XchP<NW> xch;
     __shared__ unsigned int item_sh;
     const TArgs &a = f.t;
     const int64_t tiles = f.ntx * f.nty;
@@ -686,12 +710,26 @@ __global__ __launch_bounds__(64 * NW, BYTE ? 4 : 6) void tflow_kernel(FArgs f) {
         __syncthreads();
         const uint8_t *in = (p & 1) ? a.out : a.in;
         uint8_t *out = const_cast<uint8_t *>((p & 1) ? a.in : a.out);
-        tile_body<BYTE, R, GK, WRAPX, WRAPY, FLOW, NW>(a, in, out, tx, ty, xch);
+        tile_body_bit<R, WRAPX, WRAPY, FLOW, NW>(a, in, out, tx, ty, xch);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
         __syncthreads();
         prev_flag = f.done + ty * f.ntx + tx;
         prev_val = p + 1;
     }
+}
+
+// Natural 32-cell word j of a bit-encoded row (bit k = cell 32j + k) from
+// the pair layout and back: the even / odd halves are 16-bit halves of the
+// pair's E / O dwords.  Small-grid kernels work in natural words inside the
+// CU and convert once per launch.
+__device__ __forceinline__ uint32_t load_nat32(const uint8_t *row, int64_t j) {
+    const uint16_t *h = reinterpret_cast<const uint16_t *>(row) + 4 * (j >> 1) + (j & 1);
+    return nat32(h[0], h[2]);
+}
+__device__ __forceinline__ void store_nat32(uint8_t *row, int64_t j, uint32_t x) {
+    uint16_t *h = reinterpret_cast<uint16_t *>(row) + 4 * (j >> 1) + (j & 1);
+    h[0] = (uint16_t)compact16(x);
+    h[2] = (uint16_t)compact16(x >> 1);
 }
 
 // ------------------------------------------------------------------ small grids
@@ -725,7 +763,7 @@ __global__ __launch_bounds__(kSmallThreads) void small_kernel(SArgs a) {
         const uint8_t *row = a.in + (int64_t)(y + a.ya) * a.pitch + a.xoff;
         uint32_t v = 0;
         if (a.bit) {
-            v = reinterpret_cast<const uint32_t *>(row)[j];
+            v = load_nat32(row, j);
         } else {
             for (int k = 0; k < 32 && 32 * j + k < w; ++k) v |= (uint32_t)(row[32 * j + k] != 0) << k;
         }
@@ -782,7 +820,7 @@ __global__ __launch_bounds__(kSmallThreads) void small_kernel(SArgs a) {
         uint8_t *row = a.out + (int64_t)(y + a.ya) * a.pitch + a.xoff;
         const uint32_t v = A[i];
         if (a.bit) {
-            reinterpret_cast<uint32_t *>(row)[jj] = v;
+            store_nat32(row, jj, v);
         } else {
             for (int k = 0; k < 32 && 32 * jj + k < w; ++k) row[32 * jj + k] = (uint8_t)((v >> k) & 1u);
         }
@@ -866,7 +904,7 @@ __global__ __launch_bounds__(kRegThreads) void rsmall_kernel(RArgs a) {
             }
             const uint8_t *row = a.in + (gy + a.ya) * a.pitch + a.xoff;
             if (a.bit) {
-                x = reinterpret_cast<const uint32_t *>(row)[j];
+                x = load_nat32(row, j);
             } else {
                 for (int k = 0; k < 32 && 32 * j + k < a.w; ++k) x |= (uint32_t)(row[32 * j + k] != 0) << k;
             }
@@ -926,7 +964,7 @@ __global__ __launch_bounds__(kRegThreads) void rsmall_kernel(RArgs a) {
         uint8_t *row = a.out + (gy + a.ya) * a.pitch + a.xoff;
         const uint32_t x = v[r] & keep;
         if (a.bit) {
-            reinterpret_cast<uint32_t *>(row)[j] = x;
+            store_nat32(row, j, x);
         } else {
             for (int k = 0; k < 32 && 32 * j + k < a.w; ++k) row[32 * j + k] = (uint8_t)((x >> k) & 1u);
         }
@@ -957,42 +995,53 @@ hipError_t launch_rs(const RArgs &a, int R, unsigned blocks, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------ cell access
-// Byte: cell x of a padded row at row[xoff + x].  Bit: word (x >> 5) (floor)
-// of the dword array starting at row + xoff, bit (x & 31).
+// Byte: cell x of a padded row at row[xoff + x].  Bit: the pair layout
+// (life_bitops.h): bit pair_bit(x) of dword pair_dword(x) counted from
+// row + xoff (x may be negative: the left apron).
 __device__ __forceinline__ uint32_t get_cell(const uint8_t *row, int64_t xoff, int64_t x, bool bit) {
     if (!bit) return row[xoff + x];
     const uint32_t *w = reinterpret_cast<const uint32_t *>(row + xoff);
-    return (w[x >> 5] >> (x & 31)) & 1u;
+    return (w[pair_dword(x)] >> pair_bit(x)) & 1u;
 }
 __device__ __forceinline__ void set_cell(uint8_t *row, int64_t xoff, int64_t x, uint32_t v, bool bit) {
     if (!bit) {
         row[xoff + x] = (uint8_t)v;
         return;
     }
-    uint32_t *w = reinterpret_cast<uint32_t *>(row + xoff);
-    const uint32_t m = 1u << (x & 31);
-    w[x >> 5] = (w[x >> 5] & ~m) | (v ? m : 0u);
+    uint32_t *w = reinterpret_cast<uint32_t *>(row + xoff) + pair_dword(x);
+    const uint32_t m = 1u << pair_bit(x);
+    *w = (*w & ~m) | (v ? m : 0u);
 }
 
 // Column halo staging.  Cell columns (xapron == 1): one byte 0/1 per row.
-// 32-cell columns (temporal layouts, xapron == 32): the bit encoding sends
-// one dword per row and side, the byte encoding 32 bytes.  The left column
-// (cells [0, 32)) is word 0; the right one (cells [w-32, w)) and the right
-// apron (cells [w, w+32)) straddle two words when w % 32 != 0: a funnel shift
-// on the way out, a bit merge that keeps the owned cells on the way in.
-__device__ __forceinline__ uint32_t right_column_bits(const uint32_t *wd, int64_t w) {
-    const int64_t x = w - 32;  // w >= 32
-    return __builtin_amdgcn_alignbit(wd[(w - 1) >> 5], wd[x >> 5], (uint32_t)(x & 31));
+// Temporal layouts: the bit encoding's x-apron is one pair (64 cells, 8 B
+// per row and side, sent in pair form), the byte encoding's 32 byte cells.
+// The left column (cells [0, 64)) is pair 0; the right one (cells [w-64,
+// w)) and the right apron (cells [w, w+64)) straddle two pairs when w % 64 !=
+// 0: they go through the natural 64-bit order (nat64 / pair_of), a funnel
+// shift on the way out, a merge that keeps the owned cells on the way in.
+__device__ __forceinline__ uint64_t pair_nat(const uint32_t *wd, int64_t p) { return nat64(wd[2 * p], wd[2 * p + 1]); }
+__device__ __forceinline__ void put_pair(uint32_t *wd, int64_t p, uint64_t v) {
+    const uint2 q = pair_of(v);
+    wd[2 * p] = q.x;
+    wd[2 * p + 1] = q.y;
 }
-__device__ __forceinline__ void put_right_apron_bits(uint32_t *wd, int64_t w, uint32_t v) {
-    const uint32_t s = (uint32_t)(w & 31);
-    uint32_t *q = wd + (w >> 5);
+__device__ __forceinline__ uint64_t right_column_bits(const uint32_t *wd, int64_t w) {  // cells [w-64, w), w >= 64
+    const int64_t x = w - 64, p = x >> 6;
+    const uint32_t s = (uint32_t)(x & 63);
+    if (s == 0) return pair_nat(wd, p);
+    return (pair_nat(wd, p) >> s) | (pair_nat(wd, p + 1) << (64 - s));
+}
+__device__ __forceinline__ void put_right_apron_bits(uint32_t *wd, int64_t w, uint64_t v) {  // cells [w, w+64)
+    const int64_t p = w >> 6;
+    const uint32_t s = (uint32_t)(w & 63);
     if (s == 0) {
-        q[0] = v;
+        put_pair(wd, p, v);
         return;
     }
-    q[0] = (q[0] & ((1u << s) - 1u)) | (v << s);
-    q[1] = v >> (32u - s);  // cells beyond w+31: never read as owned
+    const uint64_t keep = (1ull << s) - 1ull;  // the owned cells of the partial pair
+    put_pair(wd, p, (pair_nat(wd, p) & keep) | (v << s));
+    put_pair(wd, p + 1, v >> (64 - s));  // cells beyond w+63: never read as owned
 }
 __device__ __forceinline__ void copy32(uint8_t *dst, const uint8_t *src) {
     // byte-cell columns need not be 4-byte aligned (w % 4 != 0)
@@ -1004,10 +1053,12 @@ __global__ void pack_columns_kernel(const uint8_t *buf, int64_t pitch, int64_t y
     const int64_t y = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (y >= h) return;
     const uint8_t *row = buf + (y + ya) * pitch;
-    if (xa == 32 && bit) {
+    if (xa == 64 && bit) {
         const uint32_t *wd = reinterpret_cast<const uint32_t *>(row + xoff);
-        reinterpret_cast<uint32_t *>(stage)[y] = right_column_bits(wd, w);
-        reinterpret_cast<uint32_t *>(stage)[h + y] = wd[0];
+        uint64_t *st = reinterpret_cast<uint64_t *>(stage);
+        const uint2 r = pair_of(right_column_bits(wd, w));
+        st[y] = (uint64_t)r.x | ((uint64_t)r.y << 32);
+        st[h + y] = *reinterpret_cast<const uint64_t *>(wd);  // pair 0
         return;
     }
     if (xa == 32) {  // 32 byte cells per row and side
@@ -1027,10 +1078,12 @@ __global__ void unpack_columns_kernel(uint8_t *buf, int64_t pitch, int64_t ya, i
     const int64_t y = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (y >= h) return;
     uint8_t *row = buf + (y + ya) * pitch;
-    if (xa == 32 && bit) {
+    if (xa == 64 && bit) {
         uint32_t *wd = reinterpret_cast<uint32_t *>(row + xoff);
-        wd[-1] = reinterpret_cast<const uint32_t *>(stage)[y];
-        put_right_apron_bits(wd, w, reinterpret_cast<const uint32_t *>(stage)[h + y]);
+        const uint64_t *st = reinterpret_cast<const uint64_t *>(stage);
+        reinterpret_cast<uint64_t *>(wd)[-1] = st[y];  // pair -1 = cells [-64, 0)
+        const uint64_t r = st[h + y];
+        put_right_apron_bits(wd, w, nat64((uint32_t)r, (uint32_t)(r >> 32)));
         return;
     }
     if (xa == 32) {
@@ -1046,8 +1099,9 @@ __global__ void unpack_columns_kernel(uint8_t *buf, int64_t pitch, int64_t ya, i
 }
 
 // Periodic x inside one shard of a temporal layout whose width is not a
-// multiple of 32 (the stencil's WRAPX reads whole words): the shard is its own
-// left and right neighbour, so the aprons are filled from its own columns.
+// multiple of the lane column (64 bit cells / 32 byte cells; the tiles' WRAPX
+// reads whole lane columns): the shard is its own left and right neighbour,
+// so the aprons are filled from its own columns.
 __global__ void wrap_columns_kernel(uint8_t *buf, int64_t pitch, int64_t ya, int64_t xoff, int64_t w, int64_t h,
                                     bool bit) {
     const int64_t y = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1055,8 +1109,8 @@ __global__ void wrap_columns_kernel(uint8_t *buf, int64_t pitch, int64_t ya, int
     uint8_t *row = buf + (y + ya) * pitch;
     if (bit) {
         uint32_t *wd = reinterpret_cast<uint32_t *>(row + xoff);
-        const uint32_t l = wd[0], r = right_column_bits(wd, w);
-        wd[-1] = r;
+        const uint64_t l = pair_nat(wd, 0), r = right_column_bits(wd, w);
+        put_pair(wd, -1, r);
         put_right_apron_bits(wd, w, l);
         return;
     }
@@ -1081,7 +1135,7 @@ __global__ void import_kernel(const uint8_t *dense, uint8_t *buf, int64_t pitch,
         if (CPU == 16)
             word[k >> 2] |= v << (8 * (k & 3));
         else
-            word[k >> 5] |= v << (k & 31);
+            word[pair_dword(k)] |= v << pair_bit(k);  // a unit = two interleaved pairs
     }
     *reinterpret_cast<uint4 *>(buf + (y + ya) * pitch + xoff + 16 * u) =
         make_uint4(word[0], word[1], word[2], word[3]);
@@ -1101,7 +1155,7 @@ __global__ void export_kernel(const uint8_t *buf, uint8_t *dense, int64_t pitch,
         const int64_t x = x0 + k;
         if (x >= w) break;
         o[x] = CPU == 16 ? (uint8_t)((word[k >> 2] >> (8 * (k & 3))) & 0xFFu)
-                         : (uint8_t)((word[k >> 5] >> (k & 31)) & 1u);
+                         : (uint8_t)((word[pair_dword(k)] >> pair_bit(k)) & 1u);
     }
 }
 
@@ -1125,7 +1179,10 @@ __global__ void vtk_kernel(const uint8_t *buf, int64_t pitch, int64_t ya, int64_
         const uint8_t *row = buf + (y + ya) * pitch + xoff;
         uint32_t c;  // cell k at bit k
         if (BIT) {
-            c = row[x0 >> 3];  // x0 is a multiple of 8: one byte of the little-endian words
+            // x0 is a multiple of 8: four even cells from E, four odd from O
+            const uint32_t *wd = reinterpret_cast<const uint32_t *>(row) + 2 * (x0 >> 6);
+            const uint32_t sh = (uint32_t)((x0 & 63) >> 1);
+            c = nat32((wd[0] >> sh) & 15u, (wd[1] >> sh) & 15u);
         } else {
             c = 0;
             for (int k = 0; k < n; ++k) c |= (uint32_t)(row[x0 + k] & 1u) << k;
@@ -1148,8 +1205,8 @@ __global__ void vtk_kernel(const uint8_t *buf, int64_t pitch, int64_t ya, int64_
 // global column x0; with s = x0 & 7 its cells land at bits s.. of its first
 // output byte, so output byte j holds block cells 8j - s .. 8j - s + 7 (those
 // outside [0, w) are 0: the host ORs the bytes two blocks share).  One thread
-// per output byte; 2-D grid, y strides rows.  Bit encoding: the cells are
-// already little-endian bits, a funnel shift of two words.
+// per output byte; 2-D grid, y strides rows.  Bit encoding: the pair(s)
+// holding the byte's cells in natural order (nat64), then a funnel shift.
 template <bool BIT>
 __global__ void bits_kernel(const uint8_t *buf, int64_t pitch, int64_t ya, int64_t xoff, int64_t w, int64_t h,
                             int s, uint8_t *out, int64_t rb) {
@@ -1165,10 +1222,14 @@ __global__ void bits_kernel(const uint8_t *buf, int64_t pitch, int64_t ya, int64
         if (BIT) {
             const uint32_t *wd = reinterpret_cast<const uint32_t *>(row);
             if (c0 < 0) {
-                v = wd[0] << lo;
+                v = (uint32_t)pair_nat(wd, 0) << lo;
             } else {
-                const int64_t k = c0 >> 5;  // the next word is owned or x-apron / pitch padding: in-row
-                v = __builtin_amdgcn_alignbit(wd[k + 1], wd[k], (uint32_t)(c0 & 31));
+                // the next pair is owned or x-apron / pitch padding: in-row
+                const int64_t pp = c0 >> 6;
+                const uint32_t sh = (uint32_t)(c0 & 63);
+                uint64_t n = pair_nat(wd, pp) >> sh;
+                if (sh > 56) n |= pair_nat(wd, pp + 1) << (64 - sh);
+                v = (uint32_t)n;
             }
         } else {
             v = 0;
@@ -1202,7 +1263,7 @@ __global__ void fill_random_kernel(uint8_t *buf, int64_t pitch, int64_t ya, int6
         if (CPU == 16)
             word[k >> 2] |= v << (8 * (k & 3));
         else
-            word[k >> 5] |= v << (k & 31);
+            word[pair_dword(k)] |= v << pair_bit(k);
     }
     *reinterpret_cast<uint4 *>(buf + (y + ya) * pitch + xoff + 16 * u) =
         make_uint4(word[0], word[1], word[2], word[3]);
@@ -1229,10 +1290,13 @@ __global__ void census_kernel(const uint8_t *buf, int64_t pitch, int64_t ya, int
         uint32_t m[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int64_t left = valid - k * kPerWord;
-            m[k] = left <= 0 ? 0u
-                   : left >= kPerWord ? 0xFFFFFFFFu
-                   : (CPU == 16 ? (0xFFFFFFFFu >> (32 - 8 * left)) : (0xFFFFFFFFu >> (32 - left)));
+            if (CPU == 16) {
+                const int64_t left = valid - k * kPerWord;
+                m[k] = left <= 0 ? 0u : left >= kPerWord ? 0xFFFFFFFFu : (0xFFFFFFFFu >> (32 - 8 * left));
+            } else {  // dword k: cells 64 (k >> 1) + 2i + (k & 1), i < 32
+                const int64_t n = (valid - 64 * (k >> 1) - (k & 1) + 1) >> 1;  // valid bits (floor; may be < 0)
+                m[k] = n <= 0 ? 0u : n >= 32 ? 0xFFFFFFFFu : (0xFFFFFFFFu >> (32 - n));
+            }
         }
         for (int64_t y = blockIdx.y; y < h; y += gridDim.y) {
             const uint4 q = *reinterpret_cast<const uint4 *>(buf + (y + ya) * pitch + xoff + 16 * u);
@@ -1245,7 +1309,8 @@ __global__ void census_kernel(const uint8_t *buf, int64_t pitch, int64_t ya, int
                 while (bits) {
                     const int b = __ffs(bits) - 1;
                     bits &= bits - 1u;
-                    sum += cell_mix(base + (uint64_t)(k * kPerWord + (CPU == 16 ? b >> 3 : b)));
+                    sum += cell_mix(base + (uint64_t)(CPU == 16 ? k * kPerWord + (b >> 3)
+                                                                : 64 * (k >> 1) + 2 * b + (k & 1)));
                 }
             }
         }
@@ -1270,11 +1335,11 @@ namespace {
 // byte R64/D2 were the fastest of {16,32,64} x {2,4,8}.
 struct Tunings {
     StepTuning t[2];  // [0] byte, [1] bit
-    // temporal stencil: register rows per wave (window = kStackWaves * rows,
-    // tile = window - 2 ghost), per encoding [byte, bit]; fastest measured at
-    // 32768^2 and 65536^2 with 20 (bit) / 32 (byte) generations per launch
-    // (profiles/r02/tile_rows.txt)
-    int nr[2] = {48, 48};
+    // temporal tiles: register rows per wave, per encoding [byte (32-cell
+    // words), bit (64-cell pairs)], and waves per bit tile workgroup
+    // (window = waves x rows, tile = window - 2 ghost rows per end)
+    int nr[2] = {48, 24};
+    int nw_bit = 8;
     Tunings() : t{{64, 2}, {16, 8}} {
         for (StepTuning &v : t) {
             if (const char *e = getenv("LIFE_STEP_ROWS")) v.rows = atoi(e);
@@ -1282,36 +1347,49 @@ struct Tunings {
         }
         if (const char *e = getenv("LIFE_TEMPORAL_ROWS")) nr[1] = atoi(e);
         if (const char *e = getenv("LIFE_TEMPORAL_ROWS_BYTE")) nr[0] = atoi(e);
+        if (const char *e = getenv("LIFE_TILE_WAVES")) nw_bit = atoi(e);
     }
 };
 Tunings &tunings() {
     static Tunings t;
     return t;
 }
-bool temporal_rows_ok(int nr) { return nr == 32 || nr == 40 || nr == 48 || nr == 56 || nr == 64 || nr == 96; }
+bool temporal_rows_ok(bool bit, int nr) {
+    return bit ? (nr == 16 || nr == 24 || nr == 32)
+               : (nr == 32 || nr == 40 || nr == 48 || nr == 56 || nr == 64 || nr == 96);
+}
+// bit tile shapes with a kernel instance (pair rows R x waves NW)
+bool bit_shape_ok(int R, int NW) {
+    return (NW == 8 && (R == 16 || R == 24 || R == 32)) || (NW == 12 && R == 24) || (NW == 16 && (R == 16 || R == 24));
+}
 }  // namespace
 
 StepTuning step_tuning(bool bit) { return tunings().t[bit ? 1 : 0]; }
 
 int temporal_rows(bool bit) {
     const int nr = tunings().nr[bit ? 1 : 0];
-    (void)bit;
-    return temporal_rows_ok(nr) ? nr : 48;
+    if (!temporal_rows_ok(bit, nr)) return bit ? 24 : 48;
+    if (bit && !bit_shape_ok(nr, tunings().nw_bit)) return 24;
+    return nr;
 }
 
+int tile_waves(bool bit) {
+    return bit && bit_shape_ok(temporal_rows(true), tunings().nw_bit) ? tunings().nw_bit : kStackWaves;
+}
 
-// Per register row and generation: bit_hsum = 1 DPP move + 2 v_alignbit + 2
-// v_bitop3 (+ 1 ds_bpermute on the LDS pipe), rule1 = 8 v_bitop3: 13; the
-// byte tiles run the drifting frame (12) and add pack (8 v_dot4 + 3 shifts)
-// and unpack (8 x bfe/mul24/and) once per row and launch.
+// VALU instructions per lane position of a tile for m generations.  Bit, per
+// pair row and generation: 2 v_alignbit + 2 full adders (4 v_bitop3) + the
+// rule for both dwords (16 v_bitop3) = 22 (+ 2 ds_bpermute on the LDS pipe);
+// byte, per word row: the drifting frame (12) plus pack (8 v_dot4 + 3
+// shifts) and unpack (8 x bfe/mul24/and) once per row and launch.
 double tstep_valu_per_tile_lane(int m, bool byte) {
-    const double per_row = byte ? 12.0 : 13.0;
-    return (double)kStackWaves * (double)temporal_rows(!byte) * (per_row * (double)m + (byte ? 35.0 : 0.0));
+    if (byte) return (double)kStackWaves * (double)temporal_rows(false) * (12.0 * (double)m + 35.0);
+    return (double)tile_waves(true) * (double)temporal_rows(true) * 22.0 * (double)m;
 }
 
 void set_temporal_rows(int kernel, int nr) {
     for (int k = 0; k < 2; k++)
-        if ((kernel < 0 || kernel == k) && temporal_rows_ok(nr)) tunings().nr[k] = nr;
+        if ((kernel < 0 || kernel == k) && temporal_rows_ok(k == 1, nr)) tunings().nr[k] = nr;
 }
 
 void set_step_tuning(int kernel, int rows, int depth) {
@@ -1378,36 +1456,68 @@ hipError_t launch_step(const life_layout &L, const uint8_t *in, uint8_t *out, ui
 }
 
 namespace {
-template <bool BYTE, int R, int GK, int NW = kStackWaves>
-hipError_t launch_t(const TArgs &a, Wrap wrap, unsigned grid, hipStream_t s) {
+template <int R, int GK>
+hipError_t launch_byte_t(const TArgs &a, Wrap wrap, unsigned grid, hipStream_t s) {
+    constexpr int NW = kStackWaves;
     constexpr unsigned kThreads = 64 * NW;
     if (wrap.x && wrap.y)
-        tstep_kernel<BYTE, R, GK, true, true, NW><<<grid, kThreads, 0, s>>>(a);
+        tstep_byte_kernel<R, GK, true, true, NW><<<grid, kThreads, 0, s>>>(a);
     else if (wrap.x)
-        tstep_kernel<BYTE, R, GK, true, false, NW><<<grid, kThreads, 0, s>>>(a);
+        tstep_byte_kernel<R, GK, true, false, NW><<<grid, kThreads, 0, s>>>(a);
     else if (wrap.y)
-        tstep_kernel<BYTE, R, GK, false, true, NW><<<grid, kThreads, 0, s>>>(a);
+        tstep_byte_kernel<R, GK, false, true, NW><<<grid, kThreads, 0, s>>>(a);
     else
-        tstep_kernel<BYTE, R, GK, false, false, NW><<<grid, kThreads, 0, s>>>(a);
+        tstep_byte_kernel<R, GK, false, false, NW><<<grid, kThreads, 0, s>>>(a);
     return hipGetLastError();
 }
 
-template <bool BYTE, int GK>
-hipError_t launch_k(const TArgs &a, Wrap wrap, unsigned grid, hipStream_t s) {
-    switch (temporal_rows(!BYTE)) {
-    case 32: return launch_t<BYTE, 32, GK>(a, wrap, grid, s);
-    case 40: return launch_t<BYTE, 40, GK>(a, wrap, grid, s);
-    case 56: return launch_t<BYTE, 56, GK>(a, wrap, grid, s);
-    case 64: return launch_t<BYTE, 64, GK>(a, wrap, grid, s);
-    case 96: return launch_t<BYTE, 96, GK>(a, wrap, grid, s);
-    default: return launch_t<BYTE, 48, GK>(a, wrap, grid, s);
+template <int GK>
+hipError_t launch_byte_k(const TArgs &a, Wrap wrap, unsigned grid, hipStream_t s) {
+    switch (temporal_rows(false)) {
+    case 32: return launch_byte_t<32, GK>(a, wrap, grid, s);
+    case 40: return launch_byte_t<40, GK>(a, wrap, grid, s);
+    case 56: return launch_byte_t<56, GK>(a, wrap, grid, s);
+    case 64: return launch_byte_t<64, GK>(a, wrap, grid, s);
+    case 96: return launch_byte_t<96, GK>(a, wrap, grid, s);
+    default: return launch_byte_t<48, GK>(a, wrap, grid, s);
     }
+}
+
+template <int R, int NW>
+hipError_t launch_bit_t(const TArgs &a, Wrap wrap, unsigned grid, hipStream_t s) {
+    constexpr unsigned kThreads = 64 * NW;
+    if (wrap.x && wrap.y)
+        tstep_bit_kernel<R, true, true, NW><<<grid, kThreads, 0, s>>>(a);
+    else if (wrap.x)
+        tstep_bit_kernel<R, true, false, NW><<<grid, kThreads, 0, s>>>(a);
+    else if (wrap.y)
+        tstep_bit_kernel<R, false, true, NW><<<grid, kThreads, 0, s>>>(a);
+    else
+        tstep_bit_kernel<R, false, false, NW><<<grid, kThreads, 0, s>>>(a);
+    return hipGetLastError();
+}
+
+// the bit tile shape's instances: per-launch tiles and the occupancy probe
+#define LIFE_BIT_SHAPES(X) X(24, 8) X(16, 8) X(32, 8) X(24, 12) X(16, 16) X(24, 16)
+hipError_t launch_bit(const TArgs &a, Wrap wrap, unsigned grid, hipStream_t s) {
+    const int R = temporal_rows(true), NW = tile_waves(true);
+#define LIFE_BIT_CASE(r, nw) \
+    if (R == r && NW == nw) return launch_bit_t<r, nw>(a, wrap, grid, s);
+    LIFE_BIT_SHAPES(LIFE_BIT_CASE)
+#undef LIFE_BIT_CASE
+    return hipErrorInvalidValue;
+}
+const void *tstep_bit_fn() {
+    const int R = temporal_rows(true), NW = tile_waves(true);
+#define LIFE_BIT_CASE(r, nw) \
+    if (R == r && NW == nw) return (const void *)tstep_bit_kernel<r, true, true, nw>;
+    LIFE_BIT_SHAPES(LIFE_BIT_CASE)
+#undef LIFE_BIT_CASE
+    return nullptr;
 }
 }  // namespace
 
 int tile_ghost(const life_layout &L, int m) { return is_bit(L) ? m : L.generations_per_exchange; }
-
-
 
 // LIFE_BANDS=0: no banded tile column (A/B knob)
 static bool bands_enabled() {
@@ -1420,17 +1530,19 @@ static bool bands_enabled() {
 
 TileGeom tile_geom(const life_layout &L, int m) {
     TileGeom g;
-    g.words = 62;
-    g.rows = (int64_t)kStackWaves * temporal_rows(is_bit(L)) - 2 * (int64_t)tile_ghost(L, m);
-    const int64_t W = (L.w + 31) / 32;
-    g.ntx = (W + g.words - 1) / g.words;
+    const bool bit = is_bit(L);
+    g.lanes = 62;
+    g.cells = bit ? 64 : 32;
+    g.rows = (int64_t)tile_waves(bit) * temporal_rows(bit) - 2 * (int64_t)tile_ghost(L, m);
+    const int64_t W = (L.w + g.cells - 1) / g.cells;  // lane columns (pairs / words) per row
+    g.ntx = (W + g.lanes - 1) / g.lanes;
     g.nty = (L.h + g.rows - 1) / g.rows;
-    // the last tile column owns o words: bands of G >= o + 2 lanes when G <= 32
-    // (65536^2: o = 2, G = 4, 16 tile rows per workgroup instead of 1)
-    const int64_t o = W - g.words * (g.ntx - 1);
+    // the last tile column owns o lane columns: bands of G >= o + 2 lanes when
+    // G <= 32 (65536^2: 1024 pairs, o = 32, no bands; 32768^2: o = 16, G = 32)
+    const int64_t o = W - g.lanes * (g.ntx - 1);
     int gsh = 2;
     while ((1 << gsh) < o + 2) ++gsh;
-    g.gsh = is_bit(L) && bands_enabled() && gsh <= 5 ? gsh : 6;
+    g.gsh = bit && bands_enabled() && gsh <= 5 ? gsh : 6;
     g.bcol = g.gsh < 6 ? g.ntx - 1 : -1;
     return g;
 }
@@ -1444,20 +1556,24 @@ static bool tail_split_enabled() {
     return on;
 }
 
-// resident workgroups of the R = 48 tiles of an encoding on this device
-// (occupancy, once): bit 3 per CU, byte 2
-static int slots_of(const void *fn) {
+// resident workgroups of a kernel on this device (occupancy)
+static int slots_of(const void *fn, int threads) {
     int dev = 0, cus = 0, per = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
+    if (!fn || hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 64 * kStackWaves, 0) != hipSuccess)
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, threads, 0) != hipSuccess)
         return 0;
     return cus * per;
 }
-static int tstep_slots(bool bit) {
-    static const int nbit = slots_of((const void *)tstep_kernel<false, 48, 0, true, true, kStackWaves>);
-    static const int nbyte = slots_of((const void *)tstep_kernel<true, 48, 32, true, true, kStackWaves>);
-    return bit ? nbit : nbyte;
+// the bit tiles of the current shape (cached per shape)
+static int tstep_bit_slots() {
+    static int cached = 0, key = -1;
+    const int k = temporal_rows(true) * 64 + tile_waves(true);
+    if (k != key) {
+        cached = slots_of(tstep_bit_fn(), 64 * tile_waves(true));
+        key = k;
+    }
+    return cached;
 }
 
 int64_t region_items(const TileGeom &g, const TileRegion &r) {
@@ -1471,24 +1587,24 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
                         int m, Wrap wrap, hipStream_t s,
                         double *valu_lane_ops) {
     const int K = L.generations_per_exchange;
-    // m <= 32: the tile's edge lanes absorb at most 32 wrong bits; m <= the
+    const bool bit = is_bit(L);
+    // m <= 32: the tile's edge lanes absorb at most 32 wrong cells; m <= the
     // apron depth a partitioned axis provides
     if (nreg < 0 || nreg > kMaxRegions || m > K || m > 32 || K < 2 || L.yapron != K ||
-        kStackWaves * temporal_rows(is_bit(L)) - 2 * tile_ghost(L, m) < 1 ||
-        (!is_bit(L) && K != 16 && K != 32))
+        tile_waves(bit) * temporal_rows(bit) - 2 * tile_ghost(L, m) < 1 || (!bit && K != 16 && K != 32))
         return hipErrorInvalidValue;
+    const TileGeom g = tile_geom(L, m);
     TArgs a;
     a.in = in;
     a.out = out;
     a.pitch = L.pitch;
     a.xoff = L.xoff;
-    a.W = (L.w + 31) / 32;  // the last word may be partial: its upper cells are the right apron
+    a.W = (L.w + g.cells - 1) / g.cells;  // the last lane column may be partial: its upper cells are the right apron
     a.h = L.h;
     a.ya = L.yapron;
     a.m = m;
     a.nreg = 0;
     a.first[0] = 0;
-    const TileGeom g = tile_geom(L, m);
     a.gsh = (int32_t)g.gsh;
     a.bcol = g.bcol;
     for (int k = 0; k < nreg; k++) {
@@ -1503,21 +1619,19 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
     if (a.nreg == 0 || m <= 0) return hipSuccess;
     int64_t items = a.first[a.nreg];  // one workgroup per tile (or banded item)
     a.half_first = a.half_y = a.half_ntx = a.half_yend = 0;
-    if (is_bit(L) && temporal_rows(true) == 48 && a.nreg == 1 && a.tx0[0] == 0 && a.tx1[0] == g.ntx &&
-        tail_split_enabled()) {
+    const int64_t T2 = (int64_t)tile_waves(bit) * (temporal_rows(bit) / 2) - 2 * (int64_t)tile_ghost(L, m);
+    if (bit && T2 >= 1 && a.nreg == 1 && a.tx0[0] == 0 && a.tx1[0] == g.ntx && tail_split_enabled()) {
         // one full-width region: the whole shard, or the interior of a row
         // strip (rows [ra, rb) of tiles; the ring runs concurrently)
         // The launch runs items / slots rounds of equal tiles; a last round
-        // under half full leaves most CUs idle for a whole tile time (bit
-        // 65536^2, 20 generations: 6315 items on 768 slots = 8.2 rounds).
+        // under half full leaves most CUs idle for a whole tile time.
         // Measured (profiles/r02/r2z): bit 20-generation calls +1.5-2 %; the
         // byte tiles (2 per CU, 32 ghost rows: a third of a half tile) lost
         // 3-4 %, so they keep whole tiles.
-        // Re-tile the bottom q tile rows as half-height tiles (R = 24, one
-        // round's worth or more): they are dispatched last, so the final round
-        // is half-length items on every slot.
-        const int slots = tstep_slots(is_bit(L));
-        const int64_t T2 = (int64_t)kStackWaves * 24 - 2 * (int64_t)tile_ghost(L, m);  // half tile: owned rows
+        // Re-tile the bottom q tile rows as half-height tiles (R / 2 rows per
+        // wave, one round's worth or more): they are dispatched last, so the
+        // final round is half-length items on every slot.
+        const int slots = tstep_bit_slots();
         const int64_t rem = slots > 0 ? items % slots : 0;
         const int64_t ty0 = a.ty0[0], ty1 = a.ty1[0], yend = std::min(ty1 * g.rows, L.h);
         if (slots > 0 && items > slots && rem != 0 && rem <= slots / 2) {
@@ -1535,55 +1649,48 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
         }
     }
     if (valu_lane_ops) {
-        const bool byte = !is_bit(L);
-        *valu_lane_ops = (double)(a.half_first > 0 ? a.half_first : items) * 64.0 * tstep_valu_per_tile_lane(m, byte);
+        *valu_lane_ops = (double)(a.half_first > 0 ? a.half_first : items) * 64.0 * tstep_valu_per_tile_lane(m, !bit);
         if (a.half_first > 0)  // half tiles: R / 2 register rows per wave
-            *valu_lane_ops += (double)(items - a.half_first) * 64.0 * 0.5 * tstep_valu_per_tile_lane(m, byte);
+            *valu_lane_ops += (double)(items - a.half_first) * 64.0 * 0.5 * tstep_valu_per_tile_lane(m, !bit);
     }
     const unsigned grid = (unsigned)items;
-    if (is_bit(L)) return launch_k<false, 0>(a, wrap, grid, s);
-    return K == 16 ? launch_k<true, 16>(a, wrap, grid, s) : launch_k<true, 32>(a, wrap, grid, s);
+    if (bit) return launch_bit(a, wrap, grid, s);
+    return K == 16 ? launch_byte_k<16>(a, wrap, grid, s) : launch_byte_k<32>(a, wrap, grid, s);
 }
 
 namespace {
-// Instances of the dataflow tiles: bit R = 40 / 48 (runtime ghost rows =
-// m), byte R = 48 with K = 16 / 32 ghost rows (compile-time, as tstep).
-template <bool BYTE, int R, int GK, int FLOW, int NW = kStackWaves>
-const void *flow_fn() {
-    return (const void *)tflow_kernel<BYTE, R, GK, true, true, FLOW, NW>;
-}
+// Instances of the dataflow tiles (bit, both axes wrapped): one per tile shape
+// and hand-off form.
 const void *flow_kernel_of(const life_layout &L, int flow) {
-    const bool f2 = flow == 2;
-    if (is_bit(L)) {
-        if (temporal_rows(true) == 40) return f2 ? flow_fn<false, 40, 0, 2>() : flow_fn<false, 40, 0, 1>();
-        if (temporal_rows(true) == 48) return f2 ? flow_fn<false, 48, 0, 2>() : flow_fn<false, 48, 0, 1>();
-        return nullptr;
-    }
-    if (temporal_rows(false) != 48) return nullptr;
-    if (L.generations_per_exchange == 16) return f2 ? flow_fn<true, 48, 16, 2>() : flow_fn<true, 48, 16, 1>();
-    if (L.generations_per_exchange == 32) return f2 ? flow_fn<true, 48, 32, 2>() : flow_fn<true, 48, 32, 1>();
+    if (!is_bit(L)) return nullptr;
+    const int R = temporal_rows(true), NW = tile_waves(true);
+#define LIFE_BIT_CASE(r, nw)                                                                \
+    if (R == r && NW == nw)                                                                 \
+        return flow == 2 ? (const void *)tflow_kernel<r, true, true, 2, nw>                 \
+                         : (const void *)tflow_kernel<r, true, true, 1, nw>;
+    LIFE_BIT_SHAPES(LIFE_BIT_CASE)
+#undef LIFE_BIT_CASE
     return nullptr;
 }
 }  // namespace
 
 bool flow_ok(const life_layout &L, int m) {
-    // an instance for this encoding / tile height / apron depth, and the
-    // dependency rule reads tile rows ty-2..ty+2: a window may reach at most
-    // one tile row beyond its neighbours (ghost rows <= T); byte tiles hold
-    // K ghost rows whatever m
+    // an instance for this encoding / tile shape, and the dependency rule
+    // reads tile rows ty-2..ty+2: a window may reach at most one tile row
+    // beyond its neighbours (ghost rows <= T)
     if (!flow_kernel_of(L, 1) || m < 1) return false;
     const TileGeom g = tile_geom(L, m);
     return g.rows >= tile_ghost(L, m);
 }
 
 int flow_slots(const life_layout &L) {
-    const void *fn = flow_kernel_of(L, 1);
-    int dev = 0, cus = 0, per = 0;
-    if (!fn || hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 64 * kStackWaves, 0) != hipSuccess)
-        return 0;
-    return cus * per;
+    static int cached = 0, key = -1;
+    const int k = is_bit(L) ? temporal_rows(true) * 64 + tile_waves(true) : -2;
+    if (k != key) {
+        cached = slots_of(flow_kernel_of(L, 1), 64 * tile_waves(is_bit(L)));
+        key = k;
+    }
+    return cached;
 }
 
 hipError_t launch_tflow(const life_layout &L, const uint8_t *in, uint8_t *out, int m, int64_t passes,
@@ -1598,7 +1705,7 @@ hipError_t launch_tflow(const life_layout &L, const uint8_t *in, uint8_t *out, i
     f.t.out = out;
     f.t.pitch = L.pitch;
     f.t.xoff = L.xoff;
-    f.t.W = (L.w + 31) / 32;
+    f.t.W = (L.w + g.cells - 1) / g.cells;
     f.t.h = L.h;
     f.t.ya = L.yapron;
     f.t.m = m;
@@ -1612,15 +1719,13 @@ hipError_t launch_tflow(const life_layout &L, const uint8_t *in, uint8_t *out, i
     hipError_t e = hipMemsetAsync(head, 0, sizeof(unsigned int), s);  // the error word is the caller's
     if (e == hipSuccess) e = hipMemsetAsync(done, 0, sizeof(unsigned int) * (size_t)(g.ntx * g.nty), s);
     if (e != hipSuccess) return e;
-    static int slots[2] = {0, 0};  // per encoding: resident workgroups (occupancy query, once)
-    int &n = slots[is_bit(L) ? 1 : 0];
-    if (n <= 0) n = flow_slots(L);
+    const int n = flow_slots(L);  // resident workgroups
     if (n <= 0) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)std::min<int64_t>(f.items, n);
     // every workgroup pulls one item past the last: the 32-bit head must not wrap
     if (f.items + (int64_t)grid > kFlowMaxHead) return hipErrorInvalidValue;
     void *args[] = {&f};
-    return hipLaunchKernel(fn, dim3(grid), dim3(64 * kStackWaves), args, 0, s);
+    return hipLaunchKernel(fn, dim3(grid), dim3(64 * tile_waves(true)), args, 0, s);
 }
 
 int reg_small_rows(const life_layout &L) {
@@ -1748,7 +1853,7 @@ hipError_t launch_pack_columns(const life_layout &L, const uint8_t *buf, uint8_t
 }
 
 hipError_t launch_wrap_columns(const life_layout &L, uint8_t *buf, hipStream_t s) {
-    if (L.xapron != 32 || L.w < 32) return hipErrorInvalidValue;
+    if (L.xapron < 32 || L.w < L.xapron) return hipErrorInvalidValue;
     wrap_columns_kernel<<<blocks_for(L.h, 256), 256, 0, s>>>(buf, L.pitch, L.yapron, L.xoff, L.w, L.h, is_bit(L));
     return hipGetLastError();
 }

@@ -77,15 +77,17 @@ static int temporal_depth(int kernel) {
     return kernel == LIFE_KERNEL_BIT ? kbit : kbyte;
 }
 
-// The temporally blocked stencil (either encoding) keeps 32-cell x-aprons
-// and K-row y-aprons: every block must be at least 32 cells wide (a neighbour,
-// or the shard itself when x wraps inside it, fills the 32 apron columns) and,
-// on a partitioned y axis, at least K rows tall.
-static bool temporal_ok(int64_t nx, int64_t ny, int dims0, int dims1, int K) {
+// The temporally blocked stencil keeps one lane column of x-apron -- 64
+// cells (one interleaved pair) for the bit encoding, 32 for the byte
+// encoding -- and K-row y-aprons: every block must be at least that wide (a
+// neighbour, or the shard itself when x wraps inside it, fills the apron
+// columns) and, on a partitioned y axis, at least K rows tall.
+static int64_t temporal_xapron(int kernel) { return kernel == LIFE_KERNEL_BIT ? 64 : 32; }
+static bool temporal_ok(int64_t nx, int64_t ny, int dims0, int dims1, int K, int64_t xa) {
     for (int k = 0; k < dims0; k++) {
         int64_t s, e;
         life_decomposition(nx, dims0, k, &s, &e);
-        if (e - s < 32) return false;
+        if (e - s < xa) return false;
     }
     if (dims1 > 1)
         for (int k = 0; k < dims1; k++) {
@@ -115,16 +117,17 @@ int life_layout_query(int64_t nx, int64_t ny, int dims0, int dims1, int rank, in
     out->coords[0] = c0;
     out->coords[1] = c1;
     const int K = temporal_depth(kernel);
-    const bool temporal = K > 1 && temporal_ok(nx, ny, dims0, dims1, K);
-    out->xapron = temporal ? 32 : 1;
+    const int64_t xa = temporal_xapron(kernel);
+    const bool temporal = K > 1 && temporal_ok(nx, ny, dims0, dims1, K, xa);
+    out->xapron = temporal ? xa : 1;
     out->yapron = temporal ? K : 1;
     out->generations_per_exchange = temporal ? K : 1;
     const int64_t cells_per_unit = kernel == LIFE_KERNEL_BIT ? 128 : 16;
     out->units = (out->w + cells_per_unit - 1) / cells_per_unit;
     out->xoff = kXoff;
-    // room for the last unit, the right apron (cell, word, or 32 byte cells)
-    // and the right extra dword; the temporal byte stencil reads whole 32-byte
-    // words up to the one holding cell w+31
+    // room for the last unit, the right apron (a cell, one 64-cell pair, or 32
+    // byte cells) and the right extra dword; the temporal byte stencil reads
+    // whole 32-byte words up to the one holding cell w+31
     out->pitch = round_up(kXoff + 16 * out->units + (temporal && kernel == LIFE_KERNEL_BYTE ? 64 : 16), 256);
     out->rows = out->h + 2 * out->yapron;
     return LIFE_OK;

@@ -46,8 +46,9 @@ OPT_FLOW_CHUNK = 8
 # LIFE_TEMPORAL_DEPTH(_BYTE): generations per halo exchange of the temporal layouts
 TEMPORAL_DEPTH = {"bit": 32, "byte": 32}
 BLOCK_GENS = {"bit": 20, "byte": 32}  # tiles: default generations per launch at most (LIFE_OPT_BLOCK_GENS)
-TEMPORAL_ROWS = {"bit": 48, "byte": 48}  # default register rows per wave of the temporal tiles
+TEMPORAL_ROWS = {"bit": 24, "byte": 48}  # default register rows per wave (bit: 64-cell pair rows)
 TILE_WAVES = {"bit": 8, "byte": 8}  # waves per tile workgroup (window = waves x rows)
+TEMPORAL_XAPRON = {"bit": 64, "byte": 32}  # x-apron of the temporal layouts: one lane column
 
 # Every symbol include/life_mi355x.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = (
@@ -221,8 +222,9 @@ def density_to_thr(density: float) -> int:
 
 
 def tune_temporal(rows: int = 0, kernel=-1) -> None:
-    """Temporal tile height: register rows per wave (32/48/64/80/96) of one
-    encoding, or of both (kernel -1)."""
+    """Temporal tile height: register rows per wave of one encoding (bit:
+    16/24/32 pair rows; byte: 32/40/48/56/64/96 word rows), or of both
+    (kernel -1: each takes the value if valid for it)."""
     _check(_lib().life_tune_temporal(kernel_id(kernel), rows), "life_tune_temporal")
 
 

@@ -13,10 +13,11 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-# nx (multiple of 32: x wraps inside the words), ny, generations, m
-# (2048 x 8000: 24 tile rows, the rotation wraps several times per call)
+# nx (multiple of 64: x wraps inside the pairs), ny, generations, m
+# (2048 x 8000: 24 tile rows, the rotation wraps several times per call;
+# 4032 = 63 pairs: a second tile column owning one pair)
 CASES = [(2048, 1000, 47, 20), (1024, 3000, 64, 16), (4096, 1100, 33, 10), (1984, 700, 90, 32), (64, 900, 25, 8),
-         (2080, 2000, 61, 12), (32, 2048, 40, 20), (2048, 8000, 41, 20)]
+         (2112, 2000, 61, 12), (128, 2048, 40, 20), (2048, 8000, 41, 20), (4032, 600, 42, 21)]
 
 
 @pytest.mark.parametrize("flow", [1, 2])
@@ -88,33 +89,14 @@ def test_flow_rejected_options(gpu):
             life.configure(gpu.OPT_FLOW, 3)
         with pytest.raises(RuntimeError):
             life.configure(gpu.OPT_FLOW_CHUNK, -1)
+        with pytest.raises(RuntimeError):  # the byte dataflow form (value | 4) was removed
+            life.configure(gpu.OPT_FLOW, 5)
 
 
-# byte encoding (LIFE_OPT_FLOW value | 4: opt-in): 16-B sc1 buffer loads /
-# stores, K ghost rows per window whatever the pass size
-@pytest.mark.parametrize("nx,ny,gens", [(2048, 1000, 70), (1024, 3000, 64), (96, 700, 33)])
-def test_flow_byte_parity(gpu, oracle, nx, ny, gens):
-    g0 = oracle.fill_random(nx, ny, seed=23, density=0.45)
-    want = oracle.life_run(g0, gens)
-    with gpu.Life(nx, ny, kernel="byte", small_grid=False) as life:
-        life.configure(gpu.OPT_FLOW, 1 | 4)
-        life.configure(gpu.OPT_BLOCK_GENS, 16)
-        life.upload(g0)
-        life.step(gens)
-        assert life.last_path() == "flow"
-        np.testing.assert_array_equal(life.gather(), want)
-
-
-def test_flow_byte_fullsize_census(gpu):
-    n, gens = 32768, 3 * 32 + 7
-    with gpu.Life(n, n, kernel="byte") as ref:
-        ref.configure(gpu.OPT_FLOW, 0)
-        ref.fill_random(8, 0.5)
-        ref.step(gens)
-        want = (ref.checksum(), ref.live_count())
-    with gpu.Life(n, n, kernel="byte") as life:
-        life.configure(gpu.OPT_FLOW, 1 | 4)
-        life.fill_random(8, 0.5)
-        life.step(gens)
-        assert life.last_path() == "flow"
-        assert (life.checksum(), life.live_count()) == want
+def test_flow_is_bit_only(gpu):
+    """The byte encoding always runs per-launch tiles (its dataflow form
+    trailed them by 13 % at 65536^2 and was removed)."""
+    with gpu.Life(2048, 1000, kernel="byte", small_grid=False, flow=1) as life:
+        life.fill_random(3, 0.5)
+        life.step(70)
+        assert life.last_path() == "tiles"

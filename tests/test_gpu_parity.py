@@ -79,16 +79,17 @@ def test_byte_equals_bit_long(gpu, oracle, nx):
 
 
 @pytest.mark.parametrize("flow", [0, 1], ids=["tiles", "flow"])
-@pytest.mark.parametrize("kernel,nx,gens", [("bit", 4096, 40), ("bit", 31, 13), ("byte", 4096, 40), ("byte", 31, 13)])
+@pytest.mark.parametrize("kernel,nx,gens", [("bit", 4096, 40), ("bit", 31, 13), ("bit", 63, 13), ("byte", 4096, 40),
+                                            ("byte", 31, 13)])
 def test_timing_stats(gpu, kernel, nx, gens, flow):
     """One timed launch per generation (one-generation kernels: a block
-    narrower than the 32-cell apron) or per up to K generations (temporal
-    kernels).  Bytes are the compulsory HBM traffic: 0.25 B (bit) / 2 B
+    narrower than the x-apron, 64 bit cells / 32 byte cells) or per up to K
+    generations (temporal kernels).  Bytes are the compulsory HBM traffic: 0.25 B (bit) / 2 B
     (byte) per cell per LAUNCH; cell-updates are cells x generations; VALU
     lane-ops are modelled for the temporal kernels only.  The dataflow tiles
     (flow, bit) count each of their passes as one launch."""
     K = gpu.TEMPORAL_DEPTH[kernel]
-    temporal = nx >= 32
+    temporal = nx >= gpu.TEMPORAL_XAPRON[kernel]
     # ceil(gens / bmax) launches of nearly equal size, bmax = K capped by
     # BLOCK_GENS (the dataflow passes: gens // bmax of bmax, here exact)
     bmax = min(K, 32, gpu.BLOCK_GENS[kernel])
@@ -110,20 +111,23 @@ def test_timing_stats(gpu, kernel, nx, gens, flow):
         assert n * b == pytest.approx(nx * 4096 * launches * (0.25 if kernel == "bit" else 2.0))
         assert n * upd == pytest.approx(nx * 4096 * gens)
         assert (valu > 0) == temporal
-        if temporal:  # 3 x ceil(4096 / (NW waves x R rows - 2m)) tiles of 62 words, 64 lanes;
-            # byte: + pack/unpack (35 ops per register row per launch)
+        if temporal:  # ceil(4096 / (NW waves x R rows - 2m)) tile rows of 62-lane tiles, 64 lanes each
             R, NW = gpu.TEMPORAL_ROWS[kernel], gpu.TILE_WAVES[kernel]
             want = 0
             for m in sizes:
                 ghost = m if kernel == "bit" else K  # byte tiles: compile-time ghost depth K
                 nty = -(-4096 // (NW * R - 2 * ghost))
-                tiles = 3 * nty
-                if kernel == "bit" and not flow and os.environ.get("LIFE_BANDS", "1") != "0":
-                    # per-launch tiles, W = 128 words: the third tile column owns 4 words -> bands of 8 lanes, 8
-                    # tile rows per workgroup (life_kernels.hip tile_geom / region_items; not in the dataflow form)
-                    tiles = 2 * nty + -(-nty // 8)
-                # 13 VALU + 1 LDS per row; byte: drifting frame, 12 VALU + 1 LDS
-                per_row = (12 if kernel == "byte" else 13) * m + (35 if kernel == "byte" else 0)
+                if kernel == "bit":
+                    # 64 pairs per row: two tile columns, the second owning 2 pairs; per-launch tiles run it as
+                    # bands of 4 lanes, 16 tile rows per workgroup (life_kernels.hip tile_geom / region_items;
+                    # not in the dataflow form)
+                    tiles = 2 * nty
+                    if not flow and os.environ.get("LIFE_BANDS", "1") != "0":
+                        tiles = nty + -(-nty // 16)
+                    per_row = 22 * m  # a pair row: 2 v_alignbit + 2 full adders + 2 rules
+                else:  # 128 words per row: three tile columns; drifting frame 12 VALU + pack/unpack 35
+                    tiles = 3 * nty
+                    per_row = 12 * m + 35
                 want += tiles * 64 * NW * R * per_row
             assert n * valu == pytest.approx(want)
 
@@ -135,14 +139,17 @@ def test_timing_stats(gpu, kernel, nx, gens, flow):
                                    # widths not a multiple of 32: the shard wraps its own x-aprons
                                    (33, 9), (63, 64), (500, 500), (1000, 37), (4016, 130), (1985, 3), (2047, 200),
                                    (256, 5000), (100, 3001)])
-@pytest.mark.parametrize("flow", [0, 5], ids=["tiles", "flow"])
+@pytest.mark.parametrize("flow", [0, 1], ids=["tiles", "flow"])
 def test_temporal_single_shard(gpu, oracle, kernel, nx, ny, flow):
-    """Blocks at least 32 cells wide take the temporally blocked kernel (up to
-    K generations per launch); runs of 1, 7, 8, 9, 20, 40 and 70 generations.
-    tiles: one launch per pass; flow: LIFE_OPT_FLOW 1 | 4, the dataflow tiles
-    for both encodings where the shard wraps x in its words (the 40- and
-    70-generation calls)."""
-    assert gpu.layout_query(nx, ny, (1, 1), 0, kernel).generations_per_exchange == gpu.TEMPORAL_DEPTH[kernel]
+    """Blocks at least one lane column wide (bit: a 64-cell pair; byte: 32
+    cells) take the temporally blocked kernel (up to K generations per
+    launch), narrower ones the one-generation kernel; runs of 1, 7, 8, 9, 20,
+    40 and 70 generations.  tiles: one launch per pass; flow: LIFE_OPT_FLOW 1,
+    the dataflow tiles (bit) where the shard wraps x in its lane columns (the
+    40- and 70-generation calls)."""
+    temporal = nx >= gpu.TEMPORAL_XAPRON[kernel]
+    assert gpu.layout_query(nx, ny, (1, 1), 0, kernel).generations_per_exchange == (
+        gpu.TEMPORAL_DEPTH[kernel] if temporal else 1)
     g0 = oracle.fill_random(nx, ny, seed=nx + 3 * ny, density=0.5)
     with gpu.Life(nx, ny, kernel=kernel, small_grid=False, flow=flow) as life:
         life.upload(g0)
@@ -164,9 +171,11 @@ def test_temporal_single_shard(gpu, oracle, kernel, nx, ny, flow):
 def test_temporal_multi_shard_local(gpu, oracle, kernel, nx, ny, shards, dims):
     """K-deep aprons through the LOCAL transport: whole-word columns, K-row
     blocks of rows, ring tiles first, interior overlapped with the exchange."""
+    K = gpu.TEMPORAL_DEPTH[kernel]
+    # a partitioned block shorter than K rows, or narrower than one lane column, takes the one-cell path
+    wide = dims[0] == 1 or nx // dims[0] >= gpu.TEMPORAL_XAPRON[kernel]
+    want = K if wide and (dims[1] == 1 or ny // dims[1] >= K) else 1
     for r in range(shards):
-        K = gpu.TEMPORAL_DEPTH[kernel]  # a partitioned block shorter than K rows takes the one-cell path
-        want = K if dims[1] == 1 or ny // dims[1] >= K else 1
         assert gpu.layout_query(nx, ny, dims, r, kernel).generations_per_exchange == want
     g0 = oracle.fill_random(nx, ny, seed=7 * shards + ny, density=0.45)
     with gpu.Life(nx, ny, shards=shards, kernel=kernel, dims=dims, transport=gpu.XPORT_LOCAL) as life:
@@ -179,8 +188,8 @@ def test_temporal_multi_shard_local(gpu, oracle, kernel, nx, ny, shards, dims):
                                           err_msg=f"after {done} generations")
 
 
-@pytest.mark.parametrize("kernel", ["bit", "byte"])
-@pytest.mark.parametrize("rows", [32, 40, 48, 56, 64, 96])
+@pytest.mark.parametrize("kernel,rows", [("bit", 16), ("bit", 24), ("bit", 32)] +
+                         [("byte", r) for r in (32, 40, 48, 56, 64, 96)])
 def test_temporal_tile_heights_agree(gpu, oracle, kernel, rows):
     nx, ny = 2048, 333
     g0 = oracle.fill_random(nx, ny, seed=rows, density=0.5)

@@ -162,15 +162,15 @@ def test_halo_plan_is_symmetric(lm, kernel, nx, ny, dims):
                                              (64, 14, (1, 2), True), (96, 64, (3, 2), True),
                                              (96, 62, (3, 2), True), (96, 30, (3, 2), True)])
 def test_temporal_mode_selection(lm, nx, ny, dims, wide):
-    """Temporal blocking needs blocks >= 32 cells wide (any width: the right
-    column and apron may straddle words) and, on a partitioned y axis, >= K
-    rows (K = 16 bit, 32 byte)."""
+    """Temporal blocking needs blocks at least one lane column wide (bit: a
+    64-cell pair, byte: 32 cells; any width: the right column and apron may
+    straddle lane columns) and, on a partitioned y axis, >= K rows."""
     for r in range(dims[0] * dims[1]):
         for kernel in ("bit", "byte"):
             L = lm.layout_query(nx, ny, dims, r, kernel)
-            K = lm.TEMPORAL_DEPTH[kernel]
-            t = wide and (dims[1] == 1 or ny // dims[1] >= K)
-            assert (L.xapron, L.yapron, L.generations_per_exchange) == ((32, K, K) if t else (1, 1, 1))
+            K, xa = lm.TEMPORAL_DEPTH[kernel], lm.TEMPORAL_XAPRON[kernel]
+            t = wide and nx // dims[0] >= xa and (dims[1] == 1 or ny // dims[1] >= K)
+            assert (L.xapron, L.yapron, L.generations_per_exchange) == ((xa, K, K) if t else (1, 1, 1))
             assert L.rows == L.h + 2 * L.yapron
             if t and kernel == "byte":  # room for the 32-byte right apron and the whole 32-byte word holding its last cell
                 assert L.pitch >= L.xoff + 32 * ((L.w + 31) // 32 + 1)
