@@ -236,7 +236,7 @@ int life_dev_set_timing(life_dev *d, int on);
 /* (option 3, the sweep stencil, was removed: slower than the tiles in every
  * measured case, profiles/r02/sweep_ab.txt) */
 /* LIFE_OPT_BLOCK_GENS: the tiled stencil's generations per launch at most
- * (1..32, capped by generations_per_exchange; 0: the default, 20 for bits
+ * (1..32, capped by generations_per_exchange; 0: the default, 12 for bits
  * and 32 for bytes, or LIFE_BLOCK_GENS from the environment).  A step call of
  * g generations runs ceil(g / max) launches of nearly equal size; a bit
  * launch of m generations holds m ghost rows above and below each tile
@@ -264,10 +264,11 @@ int life_dev_set_timing(life_dev *d, int on);
  * are identical either way.  The grid must be at least one halo deep
  * (generations_per_exchange rows). */
 #define LIFE_OPT_LOOPBACK 6
-/* LIFE_OPT_FLOW (default 1, or LIFE_FLOW from the environment): a step call
+/* LIFE_OPT_FLOW (default 0 since the pair tiles -- per-launch tiles measured
+ * 3-5 % faster, DESIGN.md §5 -- or LIFE_FLOW from the environment): a step call
  * on a single shard whose axes both wrap inside it (bit encoding, width a
  * multiple of 64) runs its whole passes of m generations (m = the block
- * size, LIFE_OPT_BLOCK_GENS) as ONE persistent launch: workgroups pull
+ * size, LIFE_OPT_BLOCK_GENS; at least 4 passes) as ONE persistent launch: workgroups pull
  * (pass, tile) items in order and a tile starts when the tiles its window
  * reads have finished the previous pass, so no pass boundary drains the chip;
  * the remainder runs as an ordinary launch.  1: write-through hand-off

@@ -109,27 +109,51 @@ struct Shard {
 
 // Tiles: generations per launch at most (the apron depth K allows up to K).
 // Bit tiles hold m ghost rows per window end, so longer launches mean more
-// ghost rows (2m of 8R) but fewer window loads / stores: 20 measured best at
-// 65536^2 (16 equal, 12 / 24 / 32 1-3 % slower; profiles/r02/block_gens.txt),
-// and a 20-generation call then runs as ONE launch.  Byte tiles are
-// HBM-bound below ~32 generations per pass: 32.  LIFE_BLOCK_GENS overrides
-// both at load time; 0 = per encoding.
+// ghost rows (2m of the 192-row pair window) but fewer window loads /
+// stores: 12 measured best at 65536^2 (992 generations: 112.3-112.9 T; 10:
+// 109.4-110.0, 14: 111.3-111.7, 16: 108.4; profiles/r03/r4g), and a
+// 20-generation call then runs as two launches of 10 (97.1-97.5 T against
+// 93.5-93.9 for one launch of 20; profiles/r03/r4d).  Byte tiles are HBM-bound below ~32 generations per
+// pass: 32.  LIFE_BLOCK_GENS overrides both at load time; 0 = per encoding.
 static const int kEnvBlockGens = [] {
     const char *e = getenv("LIFE_BLOCK_GENS");
     const int v = e ? atoi(e) : 0;
     return v >= 1 && v <= 32 ? v : 0;
 }();
-// LIFE_FLOW (0/1/2) sets LIFE_OPT_FLOW's default at load time; default 1:
-// 65536^2 95 -> 100 T, 32768^2 78 -> 90 T at 20 generations per pass
-// (profiles/r02/flow_ab.txt, flow_sweep.txt).
+// LIFE_FLOW (0/1/2) sets LIFE_OPT_FLOW's default at load time; default 0.
+// With the natural-word tiles (384-row windows, 20 generations per pass) the
+// dataflow form won (65536^2 95 -> 100 T, profiles/r02/flow_ab.txt); the
+// pair tiles are half as tall, their items half as long, and the per-item
+// queue / dependency / write-through cost now outweighs the launch tails it
+// saves: 992 generations at 65536^2, per-launch tiles 109.4-112.9 T against
+// 104.2-108.5 T for the dataflow form at every pass size 10-16
+// (profiles/r03/r4g).
 static const int kEnvFlow = [] {
     const char *e = getenv("LIFE_FLOW");
-    const int v = e ? atoi(e) : 1;
-    return v >= 0 && v <= 2 ? v : 1;
+    const int v = e ? atoi(e) : 0;
+    return v >= 0 && v <= 2 ? v : 0;
 }();
 static int default_block_gens(int kernel) {
-    return kEnvBlockGens ? kEnvBlockGens : (kernel == LIFE_KERNEL_BIT ? 20 : 32);
+    return kEnvBlockGens ? kEnvBlockGens : (kernel == LIFE_KERNEL_BIT ? 12 : 32);
 }
+// LIFE_FLOW_MIN_PASSES (measurement knob, default 4): fewest passes a call
+// runs in the dataflow form
+static const int64_t kFlowMinPasses = [] {
+    const char *e = getenv("LIFE_FLOW_MIN_PASSES");
+    const int v = e ? atoi(e) : 0;
+    return (int64_t)(v >= 2 ? v : 4);
+}();
+// How timed stencil launches are bracketed (LIFE_TIMING_MODE, measurement
+// knob): 0 one event pair around a single-stream step call's launches (the
+// default: one hipEventRecord before the first launch, none between
+// launches), 1 per launch with hipEventRecord, 2 per launch stamped by the
+// dispatch itself (hipExtLaunchKernel), 3 no events.
+enum TimingMode { kTimeCall = 0, kTimeRecord = 1, kTimeExt = 2, kTimeOff = 3 };
+static const int kEnvTimingMode = [] {
+    const char *e = getenv("LIFE_TIMING_MODE");
+    const int v = e ? atoi(e) : 0;
+    return v >= 0 && v <= 3 ? v : 0;
+}();
 
 struct life_dev {
     int64_t nx = 0, ny = 0;
@@ -149,6 +173,7 @@ struct life_dev {
     int flow = kEnvFlow;  // LIFE_OPT_FLOW: single-shard bit tiles as one persistent dataflow launch per
                           // step call (1: write-through hand-off, 2: plain stores + release; 0 off)
     int64_t flow_chunk = 0;  // LIFE_OPT_FLOW_CHUNK: passes per dataflow launch at most (0: automatic)
+    TimedLaunch *call_timer = nullptr;  // kTimeCall: the pair bracketing the current step call
     std::vector<Shard> shards;
     double acc_ms = 0.0;
     int64_t acc_launches = 0;
@@ -378,6 +403,25 @@ TimedLaunch *timer_slot(Shard &s, int *rc) {
     return &s.timers[s.timers_used++];
 }
 
+// The timer of one timed launch: kTimeCall books it into the call's pair
+// (*use_events false); the per-launch modes take a fresh pair.
+int launch_timer(life_dev *d, Shard &s, int launches, TimedLaunch **t, bool *use_events) {
+    *t = nullptr;
+    *use_events = false;
+    if (d->call_timer) {
+        d->call_timer->launches += launches;
+        *t = d->call_timer;
+        return LIFE_OK;
+    }
+    if (kEnvTimingMode == kTimeOff) return LIFE_OK;
+    int rc;
+    *t = timer_slot(s, &rc);
+    if (!*t) return rc;
+    (*t)->launches = launches;
+    *use_events = true;
+    return LIFE_OK;
+}
+
 // Launches one stencil region on `st`; when timing is on and `timed`,
 // brackets it with HIP events on that stream and books its algorithmic bytes
 // (1 B read + 1 B written per BYTE cell, 2 bits per BIT cell).
@@ -385,15 +429,14 @@ int launch_region(life_dev *d, Shard &s, const life::Region &r, bool timed, hipS
     const uint8_t *in = s.buf[s.cur];
     uint8_t *out = s.buf[s.cur ^ 1];
     TimedLaunch *t = nullptr;
+    bool ev = false;
     if (d->timing && timed) {
-        int rc;
-        t = timer_slot(s, &rc);
-        if (!t) return rc;
-        HIPCHK(hipEventRecord(t->a, st));
+        CHK(launch_timer(d, s, 1, &t, &ev));
+        if (ev) HIPCHK(hipEventRecord(t->a, st));
     }
     HIPCHK(life::launch_step(s.lay, in, out, s.sink, r, wrap_of(d), st));
-    if (t) {
-        HIPCHK(hipEventRecord(t->b, st));
+    if (d->timing && timed) {
+        if (ev) HIPCHK(hipEventRecord(t->b, st));
         const bool bit = s.lay.kernel == LIFE_KERNEL_BIT;
         const int64_t cpu = bit ? 128 : 16;
         const int64_t xa = r.u0 * cpu, xb = r.u1 * cpu < s.lay.w ? r.u1 * cpu : s.lay.w;
@@ -464,16 +507,15 @@ int launch_tiles(life_dev *d, Shard &s, const life::TileRegion *r, int nreg, int
     const uint8_t *in = s.buf[s.cur];
     uint8_t *out = s.buf[s.cur ^ 1];
     TimedLaunch *t = nullptr;
-    if (d->timing && timed) {
-        int rc;
-        t = timer_slot(s, &rc);
-        if (!t) return rc;
-        HIPCHK(hipEventRecord(t->a, st));
-    }
+    bool ev = false;
+    if (d->timing && timed) CHK(launch_timer(d, s, 1, &t, &ev));
     double valu = 0.0;
-    HIPCHK(life::launch_tstep(s.lay, in, out, r, nreg, m, wrap_of(d), st, &valu));
-    if (t) {
-        HIPCHK(hipEventRecord(t->b, st));
+    const bool ext = ev && kEnvTimingMode == kTimeExt;  // events stamped by the dispatch itself
+    if (ev && !ext) HIPCHK(hipEventRecord(t->a, st));
+    HIPCHK(life::launch_tstep(s.lay, in, out, r, nreg, m, wrap_of(d), st, &valu, ext ? t->a : nullptr,
+                              ext ? t->b : nullptr));
+    if (ev && !ext) HIPCHK(hipEventRecord(t->b, st));
+    if (d->timing && timed) {
         const life::TileGeom g = life::tile_geom(s.lay, m);
         for (int k = 0; k < nreg; k++) {
             const int64_t xa = r[k].tx0 * g.lanes * g.cells, xb = std::min(r[k].tx1 * g.lanes * g.cells, s.lay.w);
@@ -949,7 +991,10 @@ static int step_flow(life_dev *d, int64_t generations, int64_t *done) {
     int m = std::min(L.generations_per_exchange, 32);
     if (d->block_gens > 0) m = std::min(m, d->block_gens);
     const int64_t passes = generations / m;
-    if (passes < 2 || !life::flow_ok(L, m)) return LIFE_OK;
+    // a call of 2-3 passes ran 0.58 ms per 10-generation pass against 0.42 for
+    // the per-launch tiles (profiles/r03/r4d); the dataflow form pays from
+    // about 4 passes (0.474 ms per 12-generation pass in long runs)
+    if (passes < kFlowMinPasses || !life::flow_ok(L, m)) return LIFE_OK;
     const life::TileGeom g = life::tile_geom(L, m);
     const size_t words = (size_t)(2 + g.ntx * g.nty);
     if (words > s.flow_words) {
@@ -974,17 +1019,14 @@ static int step_flow(life_dev *d, int64_t generations, int64_t *done) {
     for (int64_t left = passes; left > 0;) {
         const int64_t n = std::min(left, per);
         TimedLaunch *t = nullptr;
-        if (d->timing) {
-            int rc;
-            t = timer_slot(s, &rc);
-            if (!t) return rc;
-            HIPCHK(hipEventRecord(t->a, s.stream));
-        }
+        bool ev = false;
+        if (d->timing) CHK(launch_timer(d, s, (int)n, &t, &ev));  // stats: mean per pass
+        const bool ext = ev && kEnvTimingMode == kTimeExt;
+        if (ev && !ext) HIPCHK(hipEventRecord(t->a, s.stream));
         HIPCHK(life::launch_tflow(L, s.buf[s.cur], s.buf[s.cur ^ 1], m, n, s.flow, s.flow + 2, wrap_of(d),
-                                  d->flow, s.stream));
-        if (t) {
-            HIPCHK(hipEventRecord(t->b, s.stream));
-            t->launches = (int)n;  // stats: mean per pass
+                                  d->flow, s.stream, ext ? t->a : nullptr, ext ? t->b : nullptr));
+        if (ev && !ext) HIPCHK(hipEventRecord(t->b, s.stream));
+        if (d->timing) {
             const double cells = (double)L.w * (double)L.h;
             d->acc_bytes += (double)n * cells * 0.25;
             d->acc_updates += (double)n * cells * (double)m;
@@ -997,6 +1039,8 @@ static int step_flow(life_dev *d, int64_t generations, int64_t *done) {
     *done = passes * m;
     return LIFE_OK;
 }
+
+static int step_body(life_dev *d, int64_t generations);
 
 int life_dev_step(life_dev *d, int64_t generations) {
     if (!d || generations < 0) return LIFE_EINVAL;
@@ -1015,6 +1059,26 @@ int life_dev_step(life_dev *d, int64_t generations) {
         HIPCHK(hipStreamWaitEvent(s.stream2, s.ev_entry, 0));
         HIPCHK(hipStreamWaitEvent(s.comm_stream, s.ev_entry, 0));
     }
+    // kTimeCall: one event pair around all launches of a single-stream call
+    if (d->timing && one_stream && kEnvTimingMode == kTimeCall && !small_grid(d) && temporal(d)) {
+        Shard &s = d->shards[0];
+        int rc;
+        d->call_timer = timer_slot(s, &rc);
+        if (!d->call_timer) return rc;
+        d->call_timer->launches = 0;
+        HIPCHK(hipEventRecord(d->call_timer->a, s.stream));
+        rc = step_body(d, generations);
+        TimedLaunch *t = d->call_timer;
+        d->call_timer = nullptr;
+        if (rc != LIFE_OK) return rc;
+        HIPCHK(hipEventRecord(t->b, s.stream));
+        return LIFE_OK;
+    }
+    return step_body(d, generations);
+}
+
+// The launches of one step call (life_dev_step after its entry fence).
+static int step_body(life_dev *d, int64_t generations) {
     if (small_grid(d)) {
         d->last_path = LIFE_PATH_SMALL;
         constexpr int64_t kChunk = 1 << 20;  // generations per resident launch
@@ -1066,13 +1130,25 @@ int life_dev_barrier(life_dev *d) {
     return LIFE_OK;
 }
 
+// hipStreamSynchronize, but polling the stream for the first milliseconds:
+// the blocking wait woke ~10 us after the last kernel ended (profiles/r03/r4d
+// trace), 1 % of a 20-generation 65536^2 call.
+static hipError_t wait_stream(hipStream_t st) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t e = hipStreamQuery(st);
+        if (e != hipErrorNotReady) return e;
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) return hipStreamSynchronize(st);
+    }
+}
+
 int life_dev_sync(life_dev *d) {
     if (!d) return LIFE_EINVAL;
     for (Shard &s : d->shards) {
         HIPCHK(hipSetDevice(s.device));
-        HIPCHK(hipStreamSynchronize(s.stream));
-        HIPCHK(hipStreamSynchronize(s.stream2));
-        HIPCHK(hipStreamSynchronize(s.comm_stream));
+        HIPCHK(wait_stream(s.stream));
+        HIPCHK(wait_stream(s.stream2));
+        HIPCHK(wait_stream(s.comm_stream));
         if (s.flow_used) {
             // a dataflow launch whose dependency wait timed out (a broken
             // hand-off): its result cannot be trusted
@@ -1363,6 +1439,15 @@ int life_dev_set_timing(life_dev *d, int on) {
     if (!d) return LIFE_EINVAL;
     CHK(harvest_timers(d));
     CHK(harvest_phases(d));
+    if (on)  // a few event pairs up front: no hipEventCreate inside a timed step call
+        for (Shard &s : d->shards) {
+            HIPCHK(hipSetDevice(s.device));
+            int rc = LIFE_OK;
+            while (s.timers.size() < 8 && timer_slot(s, &rc)) {
+            }
+            if (rc != LIFE_OK) return rc;
+            s.timers_used = 0;
+        }
     d->ph_ring = d->ph_int = d->ph_halo = d->ph_block = 0.0;
     d->ph_blocks = 0;
     d->timing = on != 0;

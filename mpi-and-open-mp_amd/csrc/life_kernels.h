@@ -84,13 +84,16 @@ constexpr int64_t kTemporalSlackRows = 8 * 96;
 // in `out` when passes is odd, else in `in`.
 bool flow_ok(const life_layout &L, int m);
 int flow_slots(const life_layout &L);  // resident workgroups of L's dataflow kernel on this device
+// ev0 / ev1 (optional): events stamped with the kernel dispatch's own start
+// and end (hipExtLaunchKernel) -- no event packets between launches.
 hipError_t launch_tflow(const life_layout &L, const uint8_t *in, uint8_t *out, int m, int64_t passes,
-                        unsigned int *head, unsigned int *done, Wrap wrap, int flow, hipStream_t s);
+                        unsigned int *head, unsigned int *done, Wrap wrap, int flow, hipStream_t s,
+                        hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // Up to 4 disjoint tile regions in one launch; *valu_lane_ops (optional):
 // the modelled VALU lane-ops of the launch as tiled (tstep_valu_per_tile_lane).
 hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, const TileRegion *r, int nreg,
                         int m, Wrap wrap, hipStream_t s,
-                        double *valu_lane_ops = nullptr);
+                        double *valu_lane_ops = nullptr, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 int temporal_rows(bool bit);      // register rows per wave: bit pair rows 16/24/32, byte word rows 32..96
 int tile_waves(bool bit);         // waves per tile workgroup: bit 8/12/16 (LIFE_TILE_WAVES), byte 8
 // VALU instructions the lanes at one lane position of a tile's waves issue

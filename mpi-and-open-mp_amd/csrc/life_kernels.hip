@@ -24,6 +24,8 @@
 #include "life_kernels.h"
 #include "life_bitops.h"
 
+#include <hip/hip_ext.h>
+
 #include <algorithm>
 #include <stdint.h>
 #include <stdlib.h>
@@ -1456,65 +1458,57 @@ hipError_t launch_step(const life_layout &L, const uint8_t *in, uint8_t *out, ui
 }
 
 namespace {
+// One launch; with events (timing on) through hipExtLaunchKernel, which
+// stamps them with the dispatch's own start and end: no event packets
+// between back-to-back launches (each cost a ~5 us bubble and ~6 us of host
+// time before the first launch, profiles/r03/r4d trace).
+hipError_t launch_fn(const void *fn, unsigned grid, unsigned threads, void *arg, hipStream_t s, hipEvent_t ev0,
+                     hipEvent_t ev1) {
+    void *args[] = {arg};
+    if (ev0 || ev1) return hipExtLaunchKernel(fn, dim3(grid), dim3(threads), args, 0, s, ev0, ev1, 0);
+    return hipLaunchKernel(fn, dim3(grid), dim3(threads), args, 0, s);
+}
+
 template <int R, int GK>
-hipError_t launch_byte_t(const TArgs &a, Wrap wrap, unsigned grid, hipStream_t s) {
+const void *byte_fn(Wrap wrap) {
     constexpr int NW = kStackWaves;
-    constexpr unsigned kThreads = 64 * NW;
-    if (wrap.x && wrap.y)
-        tstep_byte_kernel<R, GK, true, true, NW><<<grid, kThreads, 0, s>>>(a);
-    else if (wrap.x)
-        tstep_byte_kernel<R, GK, true, false, NW><<<grid, kThreads, 0, s>>>(a);
-    else if (wrap.y)
-        tstep_byte_kernel<R, GK, false, true, NW><<<grid, kThreads, 0, s>>>(a);
-    else
-        tstep_byte_kernel<R, GK, false, false, NW><<<grid, kThreads, 0, s>>>(a);
-    return hipGetLastError();
+    if (wrap.x && wrap.y) return (const void *)tstep_byte_kernel<R, GK, true, true, NW>;
+    if (wrap.x) return (const void *)tstep_byte_kernel<R, GK, true, false, NW>;
+    if (wrap.y) return (const void *)tstep_byte_kernel<R, GK, false, true, NW>;
+    return (const void *)tstep_byte_kernel<R, GK, false, false, NW>;
 }
 
 template <int GK>
-hipError_t launch_byte_k(const TArgs &a, Wrap wrap, unsigned grid, hipStream_t s) {
+const void *byte_k(Wrap wrap) {
     switch (temporal_rows(false)) {
-    case 32: return launch_byte_t<32, GK>(a, wrap, grid, s);
-    case 40: return launch_byte_t<40, GK>(a, wrap, grid, s);
-    case 56: return launch_byte_t<56, GK>(a, wrap, grid, s);
-    case 64: return launch_byte_t<64, GK>(a, wrap, grid, s);
-    case 96: return launch_byte_t<96, GK>(a, wrap, grid, s);
-    default: return launch_byte_t<48, GK>(a, wrap, grid, s);
+    case 32: return byte_fn<32, GK>(wrap);
+    case 40: return byte_fn<40, GK>(wrap);
+    case 56: return byte_fn<56, GK>(wrap);
+    case 64: return byte_fn<64, GK>(wrap);
+    case 96: return byte_fn<96, GK>(wrap);
+    default: return byte_fn<48, GK>(wrap);
     }
 }
 
 template <int R, int NW>
-hipError_t launch_bit_t(const TArgs &a, Wrap wrap, unsigned grid, hipStream_t s) {
-    constexpr unsigned kThreads = 64 * NW;
-    if (wrap.x && wrap.y)
-        tstep_bit_kernel<R, true, true, NW><<<grid, kThreads, 0, s>>>(a);
-    else if (wrap.x)
-        tstep_bit_kernel<R, true, false, NW><<<grid, kThreads, 0, s>>>(a);
-    else if (wrap.y)
-        tstep_bit_kernel<R, false, true, NW><<<grid, kThreads, 0, s>>>(a);
-    else
-        tstep_bit_kernel<R, false, false, NW><<<grid, kThreads, 0, s>>>(a);
-    return hipGetLastError();
+const void *bit_fn(Wrap wrap) {
+    if (wrap.x && wrap.y) return (const void *)tstep_bit_kernel<R, true, true, NW>;
+    if (wrap.x) return (const void *)tstep_bit_kernel<R, true, false, NW>;
+    if (wrap.y) return (const void *)tstep_bit_kernel<R, false, true, NW>;
+    return (const void *)tstep_bit_kernel<R, false, false, NW>;
 }
 
 // the bit tile shape's instances: per-launch tiles and the occupancy probe
 #define LIFE_BIT_SHAPES(X) X(24, 8) X(16, 8) X(32, 8) X(24, 12) X(16, 16) X(24, 16)
-hipError_t launch_bit(const TArgs &a, Wrap wrap, unsigned grid, hipStream_t s) {
+const void *bit_k(Wrap wrap) {
     const int R = temporal_rows(true), NW = tile_waves(true);
 #define LIFE_BIT_CASE(r, nw) \
-    if (R == r && NW == nw) return launch_bit_t<r, nw>(a, wrap, grid, s);
-    LIFE_BIT_SHAPES(LIFE_BIT_CASE)
-#undef LIFE_BIT_CASE
-    return hipErrorInvalidValue;
-}
-const void *tstep_bit_fn() {
-    const int R = temporal_rows(true), NW = tile_waves(true);
-#define LIFE_BIT_CASE(r, nw) \
-    if (R == r && NW == nw) return (const void *)tstep_bit_kernel<r, true, true, nw>;
+    if (R == r && NW == nw) return bit_fn<r, nw>(wrap);
     LIFE_BIT_SHAPES(LIFE_BIT_CASE)
 #undef LIFE_BIT_CASE
     return nullptr;
 }
+const void *tstep_bit_fn() { return bit_k(Wrap{true, true}); }
 }  // namespace
 
 int tile_ghost(const life_layout &L, int m) { return is_bit(L) ? m : L.generations_per_exchange; }
@@ -1584,8 +1578,7 @@ int64_t region_items(const TileGeom &g, const TileRegion &r) {
 }
 
 hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, const TileRegion *r, int nreg,
-                        int m, Wrap wrap, hipStream_t s,
-                        double *valu_lane_ops) {
+                        int m, Wrap wrap, hipStream_t s, double *valu_lane_ops, hipEvent_t ev0, hipEvent_t ev1) {
     const int K = L.generations_per_exchange;
     const bool bit = is_bit(L);
     // m <= 32: the tile's edge lanes absorb at most 32 wrong cells; m <= the
@@ -1653,9 +1646,9 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
         if (a.half_first > 0)  // half tiles: R / 2 register rows per wave
             *valu_lane_ops += (double)(items - a.half_first) * 64.0 * 0.5 * tstep_valu_per_tile_lane(m, !bit);
     }
-    const unsigned grid = (unsigned)items;
-    if (bit) return launch_bit(a, wrap, grid, s);
-    return K == 16 ? launch_byte_k<16>(a, wrap, grid, s) : launch_byte_k<32>(a, wrap, grid, s);
+    const void *fn = bit ? bit_k(wrap) : K == 16 ? byte_k<16>(wrap) : byte_k<32>(wrap);
+    if (!fn) return hipErrorInvalidValue;
+    return launch_fn(fn, (unsigned)items, 64u * (unsigned)tile_waves(bit), &a, s, ev0, ev1);
 }
 
 namespace {
@@ -1694,7 +1687,8 @@ int flow_slots(const life_layout &L) {
 }
 
 hipError_t launch_tflow(const life_layout &L, const uint8_t *in, uint8_t *out, int m, int64_t passes,
-                        unsigned int *head, unsigned int *done, Wrap wrap, int flow, hipStream_t s) {
+                        unsigned int *head, unsigned int *done, Wrap wrap, int flow, hipStream_t s, hipEvent_t ev0,
+                        hipEvent_t ev1) {
     const void *fn = flow_kernel_of(L, flow);
     if (!fn || !wrap.x || !wrap.y || m < 1 || m > 32 || m > L.generations_per_exchange || passes < 1 ||
         !flow_ok(L, m))
@@ -1724,8 +1718,7 @@ hipError_t launch_tflow(const life_layout &L, const uint8_t *in, uint8_t *out, i
     const unsigned grid = (unsigned)std::min<int64_t>(f.items, n);
     // every workgroup pulls one item past the last: the 32-bit head must not wrap
     if (f.items + (int64_t)grid > kFlowMaxHead) return hipErrorInvalidValue;
-    void *args[] = {&f};
-    return hipLaunchKernel(fn, dim3(grid), dim3(64 * tile_waves(true)), args, 0, s);
+    return launch_fn(fn, grid, 64u * (unsigned)tile_waves(true), &f, s, ev0, ev1);
 }
 
 int reg_small_rows(const life_layout &L) {

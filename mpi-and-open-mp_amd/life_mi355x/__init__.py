@@ -45,7 +45,7 @@ OPT_SMALL_GRID, OPT_OVERLAP, OPT_SMALL_WINDOW, OPT_BLOCK_GENS, OPT_LOOPBACK, OPT
 OPT_FLOW_CHUNK = 8
 # LIFE_TEMPORAL_DEPTH(_BYTE): generations per halo exchange of the temporal layouts
 TEMPORAL_DEPTH = {"bit": 32, "byte": 32}
-BLOCK_GENS = {"bit": 20, "byte": 32}  # tiles: default generations per launch at most (LIFE_OPT_BLOCK_GENS)
+BLOCK_GENS = {"bit": 12, "byte": 32}  # tiles: default generations per launch at most (LIFE_OPT_BLOCK_GENS)
 TEMPORAL_ROWS = {"bit": 24, "byte": 48}  # default register rows per wave (bit: 64-cell pair rows)
 TILE_WAVES = {"bit": 8, "byte": 8}  # waves per tile workgroup (window = waves x rows)
 TEMPORAL_XAPRON = {"bit": 64, "byte": 32}  # x-apron of the temporal layouts: one lane column

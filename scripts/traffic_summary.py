@@ -9,10 +9,13 @@ MI355X_MICROARCH.md's HBM section prescribes for gfx950:
   bit): FETCH_SIZE reports half the bytes of wide coalesced reads, so it is
   doubled; WRITE_SIZE is exact for 16-B streaming stores.
 * the temporal byte kernel moves 2 x 16 B per lane: calibrated as above;
-* the temporal bit kernel (tstep_kernel) loads and stores 4 B per lane, an
-  access width the guide lists as uncalibrated: scripts/calib_4b.hip copies
-  1 GiB with 4-B lanes and reads FETCH_SIZE = 0.500 GiB, WRITE_SIZE =
-  1.000 GiB (profiles/r01/calib_4b_*.csv), so the same x2 / x1 applies.
+* the temporal bit kernel loads and stores 4 B per lane (natural-word tiles,
+  rounds 1-2) or 8 B per lane (interleaved-pair tiles, tstep_bit_kernel,
+  round 3), access widths the guide lists as uncalibrated:
+  scripts/calib_4b.hip / calib_8b.hip copy 1 GiB with 4-B / 8-B lanes and
+  read FETCH_SIZE = 0.500 GiB, WRITE_SIZE = 1.000 GiB
+  (profiles/r01/calib_4b_*.csv, profiles/r03/calib_8b_*.csv), so the same
+  x2 / x1 applies.
 
 Only full-length launches are summarised (the median over the dispatches of
 the dominant kernel).
@@ -28,12 +31,12 @@ rnd = sys.argv[1] if len(sys.argv) > 1 else "r01"
 size = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
 d = os.path.join(ROOT, "profiles", rnd)
 
-VARIANTS = {  # variant -> (kernel-name substring, calibrated 16-B access)
-    "bit_onegen": ("step_kernel<life::(anonymous namespace)::BitEnc", True),
-    "byte_onegen": ("step_kernel<life::(anonymous namespace)::ByteEnc", True),
-    "bit_temporal": ("tstep_kernel<false", True),    # 4 B per lane (calib_4b)
-    "byte_temporal": ("tstep_kernel<true", True),    # 2 x 16 B per lane
-    "bit_flow": ("tflow_kernel<", True),             # 4 B per lane, sc1; one dispatch = PASSES[var] passes
+VARIANTS = {  # variant -> (kernel-name substrings (any round's name), calibrated access)
+    "bit_onegen": (("step_kernel<life::(anonymous namespace)::BitEnc",), True),
+    "byte_onegen": (("step_kernel<life::(anonymous namespace)::ByteEnc",), True),
+    "bit_temporal": (("tstep_bit_kernel<", "tstep_kernel<false"), True),  # 8 B (r03) / 4 B per lane (calib_8b / 4b)
+    "byte_temporal": (("tstep_byte_kernel<", "tstep_kernel<true"), True),  # 2 x 16 B per lane
+    "bit_flow": (("tflow_kernel<",), True),  # sc1; one dispatch = PASSES[var] passes
 }
 # dataflow launches run several passes per dispatch: the PMC job times a
 # 80-generation call at 20 generations per pass (profiles/r02/jobs/r2r.sh)
@@ -46,7 +49,8 @@ for var, (needle, calibrated) in VARIANTS.items():
         p = os.path.join(d, f"pmc_{c}_{var}.csv")
         if not os.path.exists(p):
             continue
-        rows = [r for r in csv.DictReader(open(p)) if needle in r["Kernel_Name"] and r["Counter_Name"] == c]
+        rows = [r for r in csv.DictReader(open(p))
+                if any(n in r["Kernel_Name"] for n in needle) and r["Counter_Name"] == c]
         if not rows:
             continue
         # the longest dispatches are the full-length launches
@@ -61,8 +65,8 @@ for var, (needle, calibrated) in VARIANTS.items():
         out[key] = round(fetch + vals["WRITE_SIZE"])
         out[key + "_detail"] = {"fetch_bytes_corrected": round(fetch), "fetch_size_raw_bytes": round(vals["FETCH_SIZE"]),
                                 "write_bytes": round(vals["WRITE_SIZE"]), "source": f"profiles/{rnd}/pmc_*_{var}.csv",
-                                "correction": "FETCH_SIZE x2 (gfx950; 16 B/lane per MI355X_MICROARCH.md, 4 B/lane "
-                                              "by scripts/calib_4b.hip)", "calibrated": True}
+                                "correction": "FETCH_SIZE x2 (gfx950; 16 B/lane per MI355X_MICROARCH.md, 4 B / 8 B "
+                                              "per lane by scripts/calib_4b.hip / calib_8b.hip)", "calibrated": True}
     else:
         out[key] = None
         out[key + "_detail"] = {"fetch_size_raw_bytes": round(vals["FETCH_SIZE"]),

@@ -16,8 +16,9 @@ pytestmark = pytest.mark.gpu
 # nx (multiple of 64: x wraps inside the pairs), ny, generations, m
 # (2048 x 8000: 24 tile rows, the rotation wraps several times per call;
 # 4032 = 63 pairs: a second tile column owning one pair)
-CASES = [(2048, 1000, 47, 20), (1024, 3000, 64, 16), (4096, 1100, 33, 10), (1984, 700, 90, 32), (64, 900, 25, 8),
-         (2112, 2000, 61, 12), (128, 2048, 40, 20), (2048, 8000, 41, 20), (4032, 600, 42, 21)]
+# (a call takes the dataflow form from 4 passes on)
+CASES = [(2048, 1000, 87, 20), (1024, 3000, 64, 16), (4096, 1100, 43, 10), (1984, 700, 135, 32), (64, 900, 37, 8),
+         (2112, 2000, 61, 12), (128, 2048, 85, 20), (2048, 8000, 81, 20), (4032, 600, 90, 21)]
 
 
 @pytest.mark.parametrize("flow", [1, 2])
@@ -62,15 +63,15 @@ def test_flow_fullsize_census(gpu, n, m, flow):
 
 def test_flow_back_to_back_and_chunked(gpu, oracle):
     """Consecutive dataflow calls on one device: odd then even
-    pass counts (buffer parity flips between calls), a changed pass size
+    pass counts (buffer parity flips between calls, 5 then 4 passes), a changed pass size
     (the scratch is reused or regrown), and a call split over several
     persistent launches (LIFE_OPT_FLOW_CHUNK: the 32-bit queue head's
     chunking, forced small) -- each stage bit-exact against the oracle."""
     nx, ny = 2048, 1000
     g = oracle.fill_random(nx, ny, seed=31, density=0.45)
-    with gpu.Life(nx, ny, kernel="bit", small_grid=False) as life:
+    with gpu.Life(nx, ny, kernel="bit", small_grid=False, flow=1) as life:
         life.upload(g)
-        for gens, m, chunk in [(47, 20, 0), (61, 20, 0), (50, 12, 0), (89, 12, 3), (100, 20, 1), (41, 10, 2)]:
+        for gens, m, chunk in [(107, 20, 0), (81, 20, 0), (50, 12, 0), (89, 12, 3), (100, 20, 1), (41, 10, 2)]:
             life.configure(gpu.OPT_BLOCK_GENS, m)
             life.configure(gpu.OPT_FLOW_CHUNK, chunk)
             life.set_timing(True)
@@ -81,6 +82,30 @@ def test_flow_back_to_back_and_chunked(gpu, oracle):
                 assert launches >= gens // m  # timed per pass, however the passes were chunked
             g = oracle.life_run(g, gens)
             np.testing.assert_array_equal(life.gather(), g, err_msg=f"{gens} generations, m={m}, chunk={chunk}")
+
+
+def test_flow_needs_four_passes(gpu, oracle):
+    """2-3 passes run as per-launch tiles (the dataflow form's start-up cost
+    is not repaid, life_dev.hip kFlowMinPasses), 4 take the dataflow form."""
+    nx, ny = 2048, 700
+    g = oracle.fill_random(nx, ny, seed=37, density=0.5)
+    with gpu.Life(nx, ny, kernel="bit", small_grid=False, flow=1) as life:
+        life.upload(g)
+        life.configure(gpu.OPT_BLOCK_GENS, 10)
+        for gens, path in [(20, "tiles"), (39, "tiles"), (40, "flow"), (45, "flow")]:
+            life.step(gens)
+            assert life.last_path() == path, gens
+            g = oracle.life_run(g, gens)
+        np.testing.assert_array_equal(life.gather(), g)
+
+
+def test_flow_default_off(gpu):
+    """Per-launch tiles are the default (LIFE_OPT_FLOW 0): the pair tiles beat
+    the dataflow form at every pass size (profiles/r03/r4g)."""
+    with gpu.Life(2048, 1000, kernel="bit", small_grid=False) as life:
+        life.fill_random(3, 0.5)
+        life.step(100)
+        assert life.last_path() == "tiles"
 
 
 def test_flow_rejected_options(gpu):

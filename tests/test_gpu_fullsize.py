@@ -146,15 +146,17 @@ def test_single_launch_tail_split(gpu, kernel, nx, ny, gens, bmax):
 def test_row_strip_interior_tail_split(gpu):
     """The interior launch of a row strip (one full-width region of tile rows
     [ra, rb) while the ring runs concurrently) takes half-height tail tiles
-    too, which stop at the region's last row: two 16384 x 32768 strips, two
+    too, which stop at the region's last row: two 16384 x 32768 strips, four
     20-generation blocks, against the single-shard dataflow tiles."""
-    nx, ny, gens = 16384, 65536, 40
+    nx, ny, gens = 16384, 65536, 80
     with gpu.Life(nx, ny, kernel="bit", flow=1) as life:
+        life.configure(gpu.OPT_BLOCK_GENS, 20)
         life.fill_random(4, 0.5)
         life.step(gens)
         assert life.last_path() == "flow"
         want = (life.checksum(), life.live_count())
     with gpu.Life(nx, ny, shards=2, dims=(1, 2), kernel="bit", transport=gpu.XPORT_LOCAL) as life:
+        life.configure(gpu.OPT_BLOCK_GENS, 20)
         life.fill_random(4, 0.5)
         life.step(gens)
         assert (life.checksum(), life.live_count()) == want
@@ -163,12 +165,12 @@ def test_row_strip_interior_tail_split(gpu):
 def test_driver_shape_65536_band_vs_oracle(gpu, oracle):
     """The headline configuration exactly as the driver's bench runs it
     (VERDICT r2, next-round item 3): 65536^2, seed 1, a 5-generation call then
-    a 20-generation call, per-launch tiles (flow 0: a 20-generation call is
-    one launch -- tail split and the last tile column's bands active), pinned
+    a 20-generation call, per-launch tiles (the 20 generations run as two
+    launches of 10 with half-height tail tiles; flow 0), pinned
     DIRECTLY to the CPU oracle (3-life/life2d.c:104-130 restated), not only to
     another HIP path.  The oracle runs a full-height band of 2048 + 2 x 64
     columns centred on the x = 0 seam -- it holds the wrap and the grid's
-    last (banded) tile column -- generated by the same counter-based
+    last tile column -- generated by the same counter-based
     generator; the band's own x wrap is wrong by at most 25 cells after 25
     generations, so its inner 2048 columns are exact and compared cell by
     cell after each call."""

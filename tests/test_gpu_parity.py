@@ -79,7 +79,7 @@ def test_byte_equals_bit_long(gpu, oracle, nx):
 
 
 @pytest.mark.parametrize("flow", [0, 1], ids=["tiles", "flow"])
-@pytest.mark.parametrize("kernel,nx,gens", [("bit", 4096, 40), ("bit", 31, 13), ("bit", 63, 13), ("byte", 4096, 40),
+@pytest.mark.parametrize("kernel,nx,gens", [("bit", 4096, 72), ("bit", 31, 13), ("bit", 63, 13), ("byte", 4096, 40),
                                             ("byte", 31, 13)])
 def test_timing_stats(gpu, kernel, nx, gens, flow):
     """One timed launch per generation (one-generation kernels: a block
@@ -87,7 +87,8 @@ def test_timing_stats(gpu, kernel, nx, gens, flow):
     generations (temporal kernels).  Bytes are the compulsory HBM traffic: 0.25 B (bit) / 2 B
     (byte) per cell per LAUNCH; cell-updates are cells x generations; VALU
     lane-ops are modelled for the temporal kernels only.  The dataflow tiles
-    (flow, bit) count each of their passes as one launch."""
+    (flow, bit: 72 generations = 6 passes of 12) count each of their passes
+    as one launch."""
     K = gpu.TEMPORAL_DEPTH[kernel]
     temporal = nx >= gpu.TEMPORAL_XAPRON[kernel]
     # ceil(gens / bmax) launches of nearly equal size, bmax = K capped by
@@ -146,7 +147,7 @@ def test_temporal_single_shard(gpu, oracle, kernel, nx, ny, flow):
     launch), narrower ones the one-generation kernel; runs of 1, 7, 8, 9, 20,
     40 and 70 generations.  tiles: one launch per pass; flow: LIFE_OPT_FLOW 1,
     the dataflow tiles (bit) where the shard wraps x in its lane columns (the
-    40- and 70-generation calls)."""
+    70-generation call: 5 passes of 12, then a 10-generation launch)."""
     temporal = nx >= gpu.TEMPORAL_XAPRON[kernel]
     assert gpu.layout_query(nx, ny, (1, 1), 0, kernel).generations_per_exchange == (
         gpu.TEMPORAL_DEPTH[kernel] if temporal else 1)
