@@ -312,8 +312,9 @@ int life_dev_phase_stats(life_dev *d, double *ring_ms, double *interior_ms, doub
                          int64_t *blocks);
 
 /* Stencil tuning for the whole process, per kernel family (-1: both): rows
- * each lane walks (16/32/64) and rows of loads kept in flight (2/4/8); 0
- * keeps the current value.  Defaults come from measurement;
+ * each lane walks (16/32/64) and rows of loads kept in flight (2/4/8, or 18
+ * = a 16-row strip's every row loaded before the first is computed; other
+ * row counts then use 4); 0 keeps the current value.  Defaults come from measurement;
  * LIFE_STEP_ROWS / LIFE_STEP_DEPTH override them at load time. */
 int life_tune(int kernel, int rows, int depth);
 

@@ -1492,7 +1492,8 @@ int life_dev_kernel_stats(life_dev *d, double *avg_ms, int64_t *launches, double
 }
 
 int life_tune(int kernel, int rows, int depth) {
-    if ((rows && rows != 16 && rows != 32 && rows != 64) || (depth && depth != 2 && depth != 4 && depth != 8) ||
+    if ((rows && rows != 16 && rows != 32 && rows != 64) ||
+        (depth && depth != 2 && depth != 4 && depth != 8 && depth != 18) ||
         kernel < -1 || kernel > LIFE_KERNEL_BIT)
         return LIFE_EINVAL;
     life::set_step_tuning(kernel, rows, depth);

@@ -97,6 +97,7 @@ struct Lane {
     uint4 pmask;        // wrap-right: where cell w sits inside this unit (last unit only)
     uint32_t pshift;    //   ... its bit/byte position within that dword
     bool pright;        // wrap-right: cell w is the right extra (w % cells_per_unit == 0)
+    bool needex;        // lanes 0 / 63 and the wrap-left unit: the extra dword is read
     bool wrapy;
 };
 
@@ -117,7 +118,10 @@ __device__ __forceinline__ RowData load_row(const Lane &c, int64_t y) {
     const uint8_t *row = row_ptr(c, y);
     RowData r;
     r.d = *reinterpret_cast<const uint4 *>(row + c.off);
-    r.ex = *reinterpret_cast<const uint32_t *>(row + c.exoff);
+    // only the lanes whose neighbour dword lies outside the wave (0, 63, the
+    // wrap-left unit) load it: one memory instruction per row instead of two
+    // for the other 62 lanes (their ex is never read: DPP takes lanes +-1)
+    r.ex = c.needex ? *reinterpret_cast<const uint32_t *>(row + c.exoff) : 0u;
     r.e0 = WRAPX ? *reinterpret_cast<const uint32_t *>(row + c.xoff) : 0u;  // one address per wave
     return r;
 }
@@ -208,6 +212,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs a) {
     c.exshift = 0;
     if (lane == 0) c.exoff = c.off - 4;
     if (lane == 63 && u < a.units) c.exoff = c.off + 16;
+    c.needex = lane == 0 || lane == 63;
     c.pmask = make_uint4(0u, 0u, 0u, 0u);
     c.pshift = 0;
     c.pright = false;
@@ -216,6 +221,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs a) {
             const int64_t wl = a.w - 1;
             c.exoff = a.xoff + E::dword_of(wl) * 4;
             c.exshift = E::top_shift(wl);
+            c.needex = true;
         }
         if (u == a.units - 1) {  // right of cell w-1 is cell 0
             const int64_t q = a.w - (a.units - 1) * E::kCellsPerUnit;  // 1 .. kCellsPerUnit
@@ -258,6 +264,12 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs a) {
 //  * tflow_kernel (bit): every pass of a step call on a single wrapped shard
 //    in one persistent launch, tiles handed from pass to pass (LIFE_OPT_FLOW).
 
+// LIFE_BP_AHEAD (build-time A/B): 1 = the bit tiles request each row's
+// neighbour dwords a row ahead of their use, 2 = the same behind a
+// scheduling fence
+#ifndef LIFE_BP_AHEAD
+#define LIFE_BP_AHEAD 0
+#endif
 constexpr int kStackWaves = 8;  // waves per byte tile workgroup (2 per SIMD; 12 measured slower, profiles/r02/r2w)
 struct TArgs {
     const uint8_t *in;
@@ -278,6 +290,10 @@ struct TArgs {
     // [half_y, half_yend), half_ntx per tile row, so the last round of a
     // launch is made of half-length items (launch_tstep)
     int64_t half_first, half_y, half_ntx, half_yend;
+    // XCD-aware order (bit, LIFE_XCD_ORDER): workgroups [0, xcd_n) are
+    // renumbered so that each XCD (blocks b, b + 8, ... share one) walks a
+    // contiguous row-major run of items; 0: dispatch order
+    int64_t xcd_n;
 };
 
 template <int NW>
@@ -411,6 +427,15 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
             ve[0] = BitEnc::rule1(ae0, ae1, pe0, pe1, ce0, ce1, ve[0]);
             vo[0] = BitEnc::rule1(ao0, ao1, po0, po1, co0, co1, vo[0]);
         }
+#if LIFE_BP_AHEAD
+        // the neighbour dwords of row r + 1 were requested one row earlier:
+        // a row of VALU work between each ds_bpermute and its use
+        uint32_t bl = 0u, br = 0u;
+        if (2 < R - 1) {
+            bl = bperm(laddr, vo[2]);
+            br = bperm(raddr, ve[2]);
+        }
+#endif
 #pragma unroll
         for (int r = 1; r < R - 1; ++r) {
             uint32_t ne0, ne1, no0, no1;
@@ -420,7 +445,21 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
                 no0 = xch[par][wi + 1][6][lane];
                 no1 = xch[par][wi + 1][7][lane];
             } else {
+#if LIFE_BP_AHEAD
+                uint32_t nbl = 0u, nbr = 0u;
+                if (r + 2 < R - 1) {
+                    nbl = bperm(laddr, vo[r + 2]);
+                    nbr = bperm(raddr, ve[r + 2]);
+                }
+#if LIFE_BP_AHEAD == 2
+                __builtin_amdgcn_sched_barrier(0);
+#endif
+                BitEnc::pair_sums(ve[r + 1], vo[r + 1], bl, br, ne0, ne1, no0, no1);
+                bl = nbl;
+                br = nbr;
+#else
                 hsum(ve[r + 1], vo[r + 1], ne0, ne1, no0, no1);
+#endif
             }
             ve[r] = BitEnc::rule1(pe0, pe1, ce0, ce1, ne0, ne1, ve[r]);
             vo[r] = BitEnc::rule1(po0, po1, co0, co1, no0, no1, vo[r]);
@@ -580,7 +619,15 @@ constexpr int bit_wpe(int NW, int R) { return NW == 16 ? (R <= 16 ? 8 : 4) : (R 
 template <int R, bool WRAPX, bool WRAPY, int NW>
 __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tstep_bit_kernel(TArgs a) {
     __shared__ XchP<NW> xch;
-    const int64_t wg = blockIdx.x;
+    int64_t wg = blockIdx.x;
+    if (wg < a.xcd_n) {
+        // the dispatcher deals blocks round-robin over the 8 XCDs: XCD x runs
+        // blocks 8k + x, here items first_x + k, so the tiles beside and below
+        // a tile share its XCD's L2 (their common ghost rows and boundary
+        // lines are fetched once); a bijection of [0, xcd_n)
+        const int64_t n = a.xcd_n, x = wg & 7, k = wg >> 3, per = n >> 3, rem = n & 7;
+        wg = (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + k;
+    }
     if (a.half_first > 0 && wg >= a.half_first) {
         const int64_t i = wg - a.half_first;
         tile_body_bit<R / 2, WRAPX, WRAPY, 0, NW>(a, a.in, a.out, i % a.half_ntx, i / a.half_ntx, xch, 6, 1,
@@ -608,7 +655,11 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tstep_bit_kernel(TArg
 template <int R, int GK, bool WRAPX, bool WRAPY, int NW>
 __global__ __launch_bounds__(64 * NW, 4) void tstep_byte_kernel(TArgs a) {
     __shared__ Xch<NW> xch;
-    const int64_t wg = blockIdx.x;
+    int64_t wg = blockIdx.x;
+    if (wg < a.xcd_n) {  // per-XCD row-major runs, as tstep_bit_kernel
+        const int64_t n = a.xcd_n, x = wg & 7, k = wg >> 3, per = n >> 3, rem = n & 7;
+        wg = (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + k;
+    }
     const int64_t nwg = a.first[a.nreg];
     if (wg >= nwg) return;
     int k = 0;
@@ -1398,7 +1449,7 @@ void set_step_tuning(int kernel, int rows, int depth) {
     for (int k = 0; k < 2; k++) {
         if (kernel >= 0 && kernel != k) continue;
         if (rows == 16 || rows == 32 || rows == 64) tunings().t[k].rows = rows;
-        if (depth == 2 || depth == 4 || depth == 8) tunings().t[k].depth = depth;
+        if (depth == 2 || depth == 4 || depth == 8 || depth == 18) tunings().t[k].depth = depth;
     }
 }
 
@@ -1417,6 +1468,9 @@ hipError_t launch_r(const StepArgs &a, int depth, bool wrapx, unsigned grid, hip
     switch (depth) {
     case 2: return launch_rd<E, R, 2>(a, wrapx, grid, s);
     case 8: return launch_rd<E, R, 8>(a, wrapx, grid, s);
+    case 18:  // R = 16 only: the lane's whole strip (16 + 2 rows) loaded before any row is computed
+        if constexpr (R == 16) return launch_rd<E, 16, 18>(a, wrapx, grid, s);
+        return launch_rd<E, R, 4>(a, wrapx, grid, s);
     default: return launch_rd<E, R, 4>(a, wrapx, grid, s);
     }
 }
@@ -1541,6 +1595,26 @@ TileGeom tile_geom(const life_layout &L, int m) {
     return g;
 }
 
+// LIFE_XCD_ORDER=0: dispatch-order bit tiles instead of per-XCD row-major
+// runs (TArgs::xcd_n).  Measured at the driver's 65536^2 call (profiles/r03/
+// r5a): FETCH_SIZE x2 0.758 -> 0.572 GB per launch, WRITE_SIZE 0.554 -> 0.539
+// GB (1.22x -> 1.035x compulsory), time within the run-to-run spread (+1 %)
+static bool xcd_order_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("LIFE_XCD_ORDER");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return on;
+}
+// LIFE_XCD_ORDER_BYTE=1: the same order for the byte tiles (A/B knob)
+static bool xcd_order_byte_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("LIFE_XCD_ORDER_BYTE");
+        return e ? atoi(e) != 0 : false;
+    }();
+    return on;
+}
+
 // LIFE_TAIL_SPLIT=0: no half-height tail tiles (A/B knob)
 static bool tail_split_enabled() {
     static const bool on = [] {
@@ -1641,6 +1715,7 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
             }
         }
     }
+    a.xcd_n = (bit ? xcd_order_enabled() : xcd_order_byte_enabled()) ? (a.half_first > 0 ? a.half_first : items) : 0;
     if (valu_lane_ops) {
         *valu_lane_ops = (double)(a.half_first > 0 ? a.half_first : items) * 64.0 * tstep_valu_per_tile_lane(m, !bit);
         if (a.half_first > 0)  // half tiles: R / 2 register rows per wave
