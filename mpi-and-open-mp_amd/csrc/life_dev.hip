@@ -952,11 +952,13 @@ static int step_small(life_dev *d, int64_t generations) {
     const life::RegWinPlan wp = win_plan(d);
     int launches = 1;
     if (wp.blocks > 0) {
-        // K generations per launch, buffers swapped per launch
+        // K generations per launch, buffers swapped per launch; between the
+        // launches of the call the grid stays in natural 32-cell words
         launches = 0;
         for (int64_t g = 0; g < generations; g += wp.K, ++launches) {
             const int m = (int)(generations - g < wp.K ? generations - g : wp.K);
-            HIPCHK(life::launch_reg_win(s.lay, wp, s.buf[s.cur], s.buf[s.cur ^ 1], m, s.stream));
+            HIPCHK(life::launch_reg_win(s.lay, wp, s.buf[s.cur], s.buf[s.cur ^ 1], m, s.stream, g > 0,
+                                        g + m < generations));
             s.cur ^= 1;
         }
     } else {

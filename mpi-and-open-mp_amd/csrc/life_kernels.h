@@ -26,6 +26,7 @@ struct StepArgs {
     int64_t pitch, xoff, units, w, h, ya;
     int64_t u0, u1, r0, r1, nbx;
     int32_t wrapy;
+    int32_t xcd;  // 1: blocks renumbered into per-XCD row-major runs (step_kernel)
 };
 
 // Wrap flags: a periodic axis that lies entirely inside the shard (dims[d]
@@ -123,8 +124,11 @@ struct RegWinPlan {
     int R, K, ns, own, blocks;
 };
 RegWinPlan reg_win_plan(const life_layout &L, int R, int K);
+// nat_in / nat_out: the launch reads / writes natural 32-cell words instead
+// of the shard's encoding (the launches inside one call; ignored, for every
+// launch alike, when a row cannot hold them)
 hipError_t launch_reg_win(const life_layout &L, const RegWinPlan &p, const uint8_t *in, uint8_t *out, int gens,
-                          hipStream_t s);
+                          hipStream_t s, bool nat_in, bool nat_out);
 
 // Column halo staging: pack writes the last xapron columns to slot 0 and the
 // first xapron columns to slot 1 (h rows each: 1 byte 0/1 per row for a cell

@@ -193,7 +193,15 @@ __device__ __forceinline__ void strip_tail(const Lane &c, int64_t ys, int n, uin
 
 template <class E, int R, int D, bool WRAPX>
 __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs a) {
-    const int64_t bx = blockIdx.x % a.nbx, by = blockIdx.x / a.nbx;
+    int64_t b = blockIdx.x;
+    if (a.xcd) {
+        // blocks b, b + 8, ... share an XCD: give each XCD a contiguous
+        // row-major run of strips, so the strips beside and below a strip
+        // (the extra dwords of lanes 0 / 63, the two halo rows) hit its L2
+        const int64_t n = (int64_t)gridDim.x, x = b & 7, k = b >> 3, per = n >> 3, rem = n & 7;
+        b = (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + k;
+    }
+    const int64_t bx = b % a.nbx, by = b / a.nbx;
     const int lane = threadIdx.x & 63;
     const int64_t wbase = a.u0 + (bx * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * 64;
     if (wbase >= a.u1) return;  // the whole wave is right of the region
@@ -264,12 +272,6 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs a) {
 //  * tflow_kernel (bit): every pass of a step call on a single wrapped shard
 //    in one persistent launch, tiles handed from pass to pass (LIFE_OPT_FLOW).
 
-// LIFE_BP_AHEAD (build-time A/B): 1 = the bit tiles request each row's
-// neighbour dwords a row ahead of their use, 2 = the same behind a
-// scheduling fence
-#ifndef LIFE_BP_AHEAD
-#define LIFE_BP_AHEAD 0
-#endif
 constexpr int kStackWaves = 8;  // waves per byte tile workgroup (2 per SIMD; 12 measured slower, profiles/r02/r2w)
 struct TArgs {
     const uint8_t *in;
@@ -427,15 +429,6 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
             ve[0] = BitEnc::rule1(ae0, ae1, pe0, pe1, ce0, ce1, ve[0]);
             vo[0] = BitEnc::rule1(ao0, ao1, po0, po1, co0, co1, vo[0]);
         }
-#if LIFE_BP_AHEAD
-        // the neighbour dwords of row r + 1 were requested one row earlier:
-        // a row of VALU work between each ds_bpermute and its use
-        uint32_t bl = 0u, br = 0u;
-        if (2 < R - 1) {
-            bl = bperm(laddr, vo[2]);
-            br = bperm(raddr, ve[2]);
-        }
-#endif
 #pragma unroll
         for (int r = 1; r < R - 1; ++r) {
             uint32_t ne0, ne1, no0, no1;
@@ -445,21 +438,7 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
                 no0 = xch[par][wi + 1][6][lane];
                 no1 = xch[par][wi + 1][7][lane];
             } else {
-#if LIFE_BP_AHEAD
-                uint32_t nbl = 0u, nbr = 0u;
-                if (r + 2 < R - 1) {
-                    nbl = bperm(laddr, vo[r + 2]);
-                    nbr = bperm(raddr, ve[r + 2]);
-                }
-#if LIFE_BP_AHEAD == 2
-                __builtin_amdgcn_sched_barrier(0);
-#endif
-                BitEnc::pair_sums(ve[r + 1], vo[r + 1], bl, br, ne0, ne1, no0, no1);
-                bl = nbl;
-                br = nbr;
-#else
                 hsum(ve[r + 1], vo[r + 1], ne0, ne1, no0, no1);
-#endif
             }
             ve[r] = BitEnc::rule1(pe0, pe1, ce0, ce1, ne0, ne1, ve[r]);
             vo[r] = BitEnc::rule1(po0, po1, co0, co1, no0, no1, vo[r]);
@@ -909,6 +888,12 @@ struct RArgs {
     int64_t pitch, xoff, ya;
     int32_t w, h, W, lgWp, gens, bit, ns;
     int32_t own, K;  // WIN: owned rows per workgroup, halo rows above/below
+    // WIN, the launches of one call: 1 = the buffer holds natural 32-cell
+    // words (bit k = cell 32j + k at row + xoff + 4j) instead of the shard's
+    // encoding -- every launch but the first reads them, every launch but the
+    // last writes them (no pair (de)interleave or byte (un)packing between
+    // launches)
+    int32_t nat_in, nat_out;
 };
 
 // ROT16 (W == Wp == 16, rows of 481..512 cells, e.g. p46gun_big): a lane
@@ -956,7 +941,9 @@ __global__ __launch_bounds__(kRegThreads) void rsmall_kernel(RArgs a) {
                 if (gy < 0) gy += a.h;
             }
             const uint8_t *row = a.in + (gy + a.ya) * a.pitch + a.xoff;
-            if (a.bit) {
+            if (WIN && a.nat_in) {
+                x = reinterpret_cast<const uint32_t *>(row)[j];
+            } else if (a.bit) {
                 x = load_nat32(row, j);
             } else {
                 for (int k = 0; k < 32 && 32 * j + k < a.w; ++k) x |= (uint32_t)(row[32 * j + k] != 0) << k;
@@ -1016,7 +1003,9 @@ __global__ __launch_bounds__(kRegThreads) void rsmall_kernel(RArgs a) {
         }
         uint8_t *row = a.out + (gy + a.ya) * a.pitch + a.xoff;
         const uint32_t x = v[r] & keep;
-        if (a.bit) {
+        if (WIN && a.nat_out) {
+            reinterpret_cast<uint32_t *>(row)[j] = x;
+        } else if (a.bit) {
             store_nat32(row, j, x);
         } else {
             for (int k = 0; k < 32 && 32 * j + k < a.w; ++k) row[32 * j + k] = (uint8_t)((x >> k) & 1u);
@@ -1384,8 +1373,9 @@ inline unsigned blocks_for(int64_t n, int b) { return (unsigned)((n + b - 1) / b
 }  // namespace
 
 namespace {
-// Measured on MI355X at 65536^2 (scripts/tune.py, profiles/): bit R16/D8 and
-// byte R64/D2 were the fastest of {16,32,64} x {2,4,8}.
+// Measured on MI355X at 65536^2 (scripts/tune.py, profiles/): byte R64/D2 the
+// fastest of {16,32,64} x {2,4,8,18}; bit R16 with the whole strip in flight
+// (D18) 1.7 % ahead of D8 (profiles/r03/r5b tune_bit1.log).
 struct Tunings {
     StepTuning t[2];  // [0] byte, [1] bit
     // temporal tiles: register rows per wave, per encoding [byte (32-cell
@@ -1393,7 +1383,7 @@ struct Tunings {
     // (window = waves x rows, tile = window - 2 ghost rows per end)
     int nr[2] = {48, 24};
     int nw_bit = 8;
-    Tunings() : t{{64, 2}, {16, 8}} {
+    Tunings() : t{{64, 2}, {16, 18}} {
         for (StepTuning &v : t) {
             if (const char *e = getenv("LIFE_STEP_ROWS")) v.rows = atoi(e);
             if (const char *e = getenv("LIFE_STEP_DEPTH")) v.depth = atoi(e);
@@ -1485,6 +1475,15 @@ hipError_t launch_e(const StepArgs &a, const StepTuning &t, bool wrapx, unsigned
 }
 }  // namespace
 
+// LIFE_XCD_ORDER_ONEGEN=0/1: per-XCD runs of one-generation strips (StepArgs::xcd; A/B knob)
+static bool onegen_xcd_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("LIFE_XCD_ORDER_ONEGEN");
+        return e ? atoi(e) != 0 : false;
+    }();
+    return on;
+}
+
 hipError_t launch_step(const life_layout &L, const uint8_t *in, uint8_t *out, uint8_t *sink,
                        const Region &reg, Wrap wrap, hipStream_t s) {
     if (reg.u1 <= reg.u0 || reg.r1 <= reg.r0) return hipSuccess;
@@ -1506,6 +1505,7 @@ hipError_t launch_step(const life_layout &L, const uint8_t *in, uint8_t *out, ui
     a.r1 = reg.r1;
     a.nbx = (reg.u1 - reg.u0 + kBlock - 1) / kBlock;
     a.wrapy = wrap.y ? 1 : 0;
+    a.xcd = onegen_xcd_enabled() ? 1 : 0;
     const int64_t nby = (reg.r1 - reg.r0 + t.rows - 1) / t.rows;
     const unsigned grid = (unsigned)(a.nbx * nby);
     return is_bit(L) ? launch_e<BitEnc>(a, t, wrap.x, grid, s) : launch_e<ByteEnc>(a, t, wrap.x, grid, s);
@@ -1606,11 +1606,13 @@ static bool xcd_order_enabled() {
     }();
     return on;
 }
-// LIFE_XCD_ORDER_BYTE=1: the same order for the byte tiles (A/B knob)
+// LIFE_XCD_ORDER_BYTE=0: dispatch order for the byte tiles.  The per-XCD
+// order measured (profiles/r03/r5b, 65536^2): 64.4-65.7 -> 66.9-67.0 T,
+// FETCH_SIZE x2 5.81 -> 5.41 GB per 32-generation launch, WRITE unchanged
 static bool xcd_order_byte_enabled() {
     static const bool on = [] {
         const char *e = getenv("LIFE_XCD_ORDER_BYTE");
-        return e ? atoi(e) != 0 : false;
+        return e ? atoi(e) != 0 : true;
     }();
     return on;
 }
@@ -1827,6 +1829,7 @@ hipError_t launch_reg_small(const life_layout &L, const uint8_t *in, uint8_t *ou
     a.ns = (int32_t)(L.h / R);
     a.own = a.h;
     a.K = 0;
+    a.nat_in = a.nat_out = 0;
     return L.w % 32 ? launch_rs<true, false>(a, R, 1, s) : launch_rs<false, false>(a, R, 1, s);
 }
 
@@ -1862,7 +1865,7 @@ RegWinPlan reg_win_plan(const life_layout &L, int R, int K) {
 }
 
 hipError_t launch_reg_win(const life_layout &L, const RegWinPlan &p, const uint8_t *in, uint8_t *out, int gens,
-                          hipStream_t s) {
+                          hipStream_t s, bool nat_in, bool nat_out) {
     if (p.blocks < 1 || gens < 1 || gens > p.K || in == out) return hipErrorInvalidValue;
     RArgs a;
     a.in = in;
@@ -1880,6 +1883,9 @@ hipError_t launch_reg_win(const life_layout &L, const RegWinPlan &p, const uint8
     a.ns = p.ns;
     a.own = p.own;
     a.K = p.K;
+    const bool fits = L.xoff + 4 * (int64_t)a.W <= L.pitch;  // natural words inside the padded row
+    a.nat_in = nat_in && fits ? 1 : 0;
+    a.nat_out = nat_out && fits ? 1 : 0;
     const unsigned b = (unsigned)p.blocks;
     return L.w % 32 ? launch_rs<true, true>(a, p.R, b, s) : launch_rs<false, true>(a, p.R, b, s);
 }

@@ -332,3 +332,28 @@ def test_gather_bits(gpu, oracle, kernel, shards, dims, nx, ny):
         want = np.packbits(dense, axis=1, bitorder="little")
         out = np.full((ny, (nx + 7) // 8), 0xA5, dtype=np.uint8)  # stale bytes must not survive
         np.testing.assert_array_equal(life.gather_bits(out), want)
+
+
+@pytest.mark.parametrize("kernel", ["byte", "bit"])
+def test_onegen_tunings(gpu, oracle, kernel):
+    """Every rows-per-lane x prefetch-depth instance of the one-generation
+    stencil (life_tune; depth 18 = a 16-row strip loaded whole, other row
+    counts then fall back to 4) on narrow blocks (4 shards of 30-31 columns:
+    one-generation layouts for both encodings) with strips cut short by the
+    block height -- bit-exact against the oracle."""
+    nx, ny = 122, 517
+    g0 = oracle.fill_random(nx, ny, seed=77, density=0.45)
+    want = oracle.life_run(g0, 5)
+    try:
+        for rows in (16, 32, 64):
+            for depth in (2, 4, 8, 18):
+                gpu.tune(rows, depth, kernel=kernel)
+                with gpu.Life(nx, ny, shards=4, kernel=kernel, dims=(4, 1), transport=gpu.XPORT_LOCAL,
+                              small_grid=False) as life:
+                    life.upload(g0)
+                    life.step(5)
+                    assert life.last_path() == "onegen"
+                    np.testing.assert_array_equal(life.gather(), want, err_msg=f"rows={rows} depth={depth}")
+    finally:
+        gpu.tune(64, 2, kernel="byte")  # the library defaults (life_kernels.hip Tunings)
+        gpu.tune(16, 18, kernel="bit")
