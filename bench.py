@@ -199,6 +199,15 @@ def main():
     if rank_mode:
         import torch.distributed as dist  # noqa: F811
 
+        if world == 1 and "RANK" not in os.environ:
+            # --rank-mode without a launcher: a world of one on this host
+            import socket
+
+            with socket.socket() as sk:
+                sk.bind(("127.0.0.1", 0))
+                port = sk.getsockname()[1]
+            os.environ.update({"RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                               "MASTER_PORT": str(port)})
         dist.init_process_group("gloo")
     n_gpus = world if world > 1 else a.gpus
     strong = a.scaling == "strong"

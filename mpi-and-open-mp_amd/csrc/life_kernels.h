@@ -69,7 +69,7 @@ TileGeom tile_geom(const life_layout &L, int m);
 // workgroups (items) one launch of region r takes: its full tiles, plus its
 // banded items when it holds the banded column
 int64_t region_items(const TileGeom &g, const TileRegion &r);
-int tile_ghost(const life_layout &L, int m);  // ghost rows per window end: m (bit) or K (byte)
+int tile_ghost(const life_layout &L, int m);  // ghost rows per window end: m (bit), K or 1 (byte, m = 1)
 // Rows a temporally blocked buffer is allocated beyond its layout's `rows`:
 // the last tile's window (<= 8 waves x 96 byte rows, 16 x 24 bit rows) may
 // read past the bottom apron without clamping.

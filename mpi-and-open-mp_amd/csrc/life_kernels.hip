@@ -1475,13 +1475,16 @@ hipError_t launch_e(const StepArgs &a, const StepTuning &t, bool wrapx, unsigned
 }
 }  // namespace
 
-// LIFE_XCD_ORDER_ONEGEN=0/1: per-XCD runs of one-generation strips (StepArgs::xcd; A/B knob)
-static bool onegen_xcd_enabled() {
-    static const bool on = [] {
+// Per-XCD runs of one-generation strips (StepArgs::xcd).  Measured at
+// 65536^2 (profiles/r03/r5f): byte 1.872 -> 1.730 ms (0.73 -> 0.79 of the copy
+// ceiling), bit 0.1998 -> 0.2012 ms (within noise, off): on for the byte
+// encoding.  LIFE_XCD_ORDER_ONEGEN=0/1 forces it for both.
+static bool onegen_xcd_enabled(bool bit) {
+    static const int v = [] {
         const char *e = getenv("LIFE_XCD_ORDER_ONEGEN");
-        return e ? atoi(e) != 0 : false;
+        return e ? (atoi(e) != 0 ? 1 : 0) : -1;
     }();
-    return on;
+    return v >= 0 ? v == 1 : !bit;
 }
 
 hipError_t launch_step(const life_layout &L, const uint8_t *in, uint8_t *out, uint8_t *sink,
@@ -1505,7 +1508,7 @@ hipError_t launch_step(const life_layout &L, const uint8_t *in, uint8_t *out, ui
     a.r1 = reg.r1;
     a.nbx = (reg.u1 - reg.u0 + kBlock - 1) / kBlock;
     a.wrapy = wrap.y ? 1 : 0;
-    a.xcd = onegen_xcd_enabled() ? 1 : 0;
+    a.xcd = onegen_xcd_enabled(is_bit(L)) ? 1 : 0;
     const int64_t nby = (reg.r1 - reg.r0 + t.rows - 1) / t.rows;
     const unsigned grid = (unsigned)(a.nbx * nby);
     return is_bit(L) ? launch_e<BitEnc>(a, t, wrap.x, grid, s) : launch_e<ByteEnc>(a, t, wrap.x, grid, s);
@@ -1565,7 +1568,21 @@ const void *bit_k(Wrap wrap) {
 const void *tstep_bit_fn() { return bit_k(Wrap{true, true}); }
 }  // namespace
 
-int tile_ghost(const life_layout &L, int m) { return is_bit(L) ? m : L.generations_per_exchange; }
+// Byte tiles are compiled for a fixed ghost depth (a runtime depth measured
+// 29 % slower, profiles/r02/ghost_ab.txt): K (16 / 32), and 1 for the
+// one-generation launches of step(1) calls at the default tile height (a
+// 384-row window then re-reads 2 rows instead of 64)
+// (LIFE_BYTE_ONE_GHOST=0: K ghost rows for them too; A/B knob)
+static bool byte_one_ghost(const life_layout &L, int m) {
+    static const bool on = [] {
+        const char *e = getenv("LIFE_BYTE_ONE_GHOST");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return on && !is_bit(L) && m == 1 && temporal_rows(false) == 48;
+}
+int tile_ghost(const life_layout &L, int m) {
+    return is_bit(L) ? m : byte_one_ghost(L, m) ? 1 : L.generations_per_exchange;
+}
 
 // LIFE_BANDS=0: no banded tile column (A/B knob)
 static bool bands_enabled() {
@@ -1723,7 +1740,10 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
         if (a.half_first > 0)  // half tiles: R / 2 register rows per wave
             *valu_lane_ops += (double)(items - a.half_first) * 64.0 * 0.5 * tstep_valu_per_tile_lane(m, !bit);
     }
-    const void *fn = bit ? bit_k(wrap) : K == 16 ? byte_k<16>(wrap) : byte_k<32>(wrap);
+    const void *fn = bit                      ? bit_k(wrap)
+                     : byte_one_ghost(L, m) ? byte_fn<48, 1>(wrap)
+                     : K == 16              ? byte_k<16>(wrap)
+                                            : byte_k<32>(wrap);
     if (!fn) return hipErrorInvalidValue;
     return launch_fn(fn, (unsigned)items, 64u * (unsigned)tile_waves(bit), &a, s, ev0, ev1);
 }
