@@ -113,6 +113,16 @@ struct RowData {
     uint32_t ex, e0;
 };
 
+// A dword every lane reads at the same address, through the VECTOR memory
+// path: the opaque zero offset keeps the compiler from turning a
+// wave-uniform address into a scalar (constant-cache) load of grid data
+// another kernel wrote.
+__device__ __forceinline__ uint32_t load_u32_vec(const uint8_t *p) {
+    uint32_t z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    return *reinterpret_cast<const uint32_t *>(p + z);
+}
+
 template <bool WRAPX>
 __device__ __forceinline__ RowData load_row(const Lane &c, int64_t y) {
     const uint8_t *row = row_ptr(c, y);
@@ -122,7 +132,7 @@ __device__ __forceinline__ RowData load_row(const Lane &c, int64_t y) {
     // wrap-left unit) load it: one memory instruction per row instead of two
     // for the other 62 lanes (their ex is never read: DPP takes lanes +-1)
     r.ex = c.needex ? *reinterpret_cast<const uint32_t *>(row + c.exoff) : 0u;
-    r.e0 = WRAPX ? *reinterpret_cast<const uint32_t *>(row + c.xoff) : 0u;  // one address per wave
+    r.e0 = WRAPX ? load_u32_vec(row + c.xoff) : 0u;  // one address per wave
     return r;
 }
 
