@@ -357,3 +357,25 @@ def test_onegen_tunings(gpu, oracle, kernel):
     finally:
         gpu.tune(64, 2, kernel="byte")  # the library defaults (life_kernels.hip Tunings)
         gpu.tune(16, 18, kernel="bit")
+
+
+@pytest.mark.parametrize("pairs,ny,gens,m", [
+    (1, 500, 9, 9), (2, 77, 11, 11), (62, 150, 13, 12), (63, 200, 13, 13), (64, 333, 20, 10), (65, 150, 7, 7),
+    (126, 100, 25, 12), (127, 190, 10, 10), (128, 64, 32, 32), (189, 90, 12, 6), (190, 40, 31, 31)])
+def test_wide_periodic_tile_columns(gpu, oracle, pairs, ny, gens, m):
+    """Bit tiles on an x axis that wraps inside the shard, several tile
+    columns of 62 pairs: widths around multiples of 62-63 pairs (a last
+    column owning 1..30 pairs runs banded, 31..62 as a whole tile), the wrap
+    seam between the last column and column 0, m up to 32 -- against the
+    oracle.  (63-pair columns with half-pair edges were measured 1.7-2.3 %
+    slower than these and dropped, profiles/r03/r5i.)"""
+    nx = 64 * pairs
+    g0 = oracle.fill_random(nx, ny, seed=pairs * 31 + ny, density=0.45)
+    want = oracle.life_run(g0, gens)
+    with gpu.Life(nx, ny, kernel="bit", small_grid=False) as life:
+        life.configure(gpu.OPT_FLOW, 0)
+        life.configure(gpu.OPT_BLOCK_GENS, m)
+        life.upload(g0)
+        life.step(gens)
+        assert life.last_path() == "tiles"
+        np.testing.assert_array_equal(life.gather(), want)
