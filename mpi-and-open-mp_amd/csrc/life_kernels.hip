@@ -302,6 +302,9 @@ struct TArgs {
     // [half_y, half_yend), half_ntx per tile row, so the last round of a
     // launch is made of half-length items (launch_tstep)
     int64_t half_first, half_y, half_ntx, half_yend;
+    // byte tiles: > 0 walks each region in strips of this many tile columns
+    // (LIFE_BYTE_STRIP)
+    int64_t strip;
     // XCD-aware order (bit, LIFE_XCD_ORDER): workgroups [0, xcd_n) are
     // renumbered so that each XCD (blocks b, b + 8, ... share one) walks a
     // contiguous row-major run of items; 0: dispatch order
@@ -655,7 +658,22 @@ __global__ __launch_bounds__(64 * NW, 4) void tstep_byte_kernel(TArgs a) {
     while (k + 1 < a.nreg && wg >= a.first[k + 1]) ++k;
     const int64_t wr = wg - a.first[k];
     const int64_t ntx = a.tx1[k] - a.tx0[k];
-    const int64_t tx = a.tx0[k] + wr % ntx, ty = a.ty0[k] + wr / ntx;
+    int64_t tx = a.tx0[k] + wr % ntx, ty = a.ty0[k] + wr / ntx;
+    if (a.strip > 0 && a.strip < ntx) {
+        // strip-major order: strips of `strip` tile columns walked down the
+        // region, so an XCD's run of items is a few columns wide and the tile
+        // below each tile (its 2K shared ghost rows) is in flight beside it
+        const int64_t C = a.strip, nty = a.ty1[k] - a.ty0[k], nfs = ntx / C, per = C * nty;
+        if (wr < nfs * per) {
+            const int64_t sI = wr / per, r = wr - sI * per;
+            ty = a.ty0[k] + r / C;
+            tx = a.tx0[k] + sI * C + r % C;
+        } else {
+            const int64_t r = wr - nfs * per, Cl = ntx - nfs * C;
+            ty = a.ty0[k] + r / Cl;
+            tx = a.tx0[k] + nfs * C + r % Cl;
+        }
+    }
     tile_body_byte<R, GK, WRAPX, WRAPY, NW>(a, a.in, a.out, tx, ty, xch);
 }
 
@@ -1383,8 +1401,10 @@ inline unsigned blocks_for(int64_t n, int b) { return (unsigned)((n + b - 1) / b
 }  // namespace
 
 namespace {
-// Measured on MI355X at 65536^2 (scripts/tune.py, profiles/): byte R64/D2 the
-// fastest of {16,32,64} x {2,4,8,18}; bit R16 with the whole strip in flight
+// Measured on MI355X at 65536^2 (scripts/tune.py, profiles/): byte R16/D8 the
+// fastest of {16,32,64} x {2,4,8} once the strips are dealt to the XCDs in
+// row-major runs (1.497 ms against 1.647 for the former R64/D2,
+// profiles/r03/r5j tune_byte1.log); bit R16 with the whole strip in flight
 // (D18) 1.7 % ahead of D8 (profiles/r03/r5b tune_bit1.log).
 struct Tunings {
     StepTuning t[2];  // [0] byte, [1] bit
@@ -1393,7 +1413,7 @@ struct Tunings {
     // (window = waves x rows, tile = window - 2 ghost rows per end)
     int nr[2] = {48, 24};
     int nw_bit = 8;
-    Tunings() : t{{64, 2}, {16, 18}} {
+    Tunings() : t{{16, 8}, {16, 18}} {
         for (StepTuning &v : t) {
             if (const char *e = getenv("LIFE_STEP_ROWS")) v.rows = atoi(e);
             if (const char *e = getenv("LIFE_STEP_DEPTH")) v.depth = atoi(e);
@@ -1644,6 +1664,16 @@ static bool xcd_order_byte_enabled() {
     return on;
 }
 
+// LIFE_BYTE_STRIP=C: byte tiles walk strips of C tile columns (A/B knob; 0 = rows)
+static int64_t byte_strip() {
+    static const int64_t c = [] {
+        const char *e = getenv("LIFE_BYTE_STRIP");
+        const int v = e ? atoi(e) : 0;
+        return (int64_t)(v > 0 ? v : 0);
+    }();
+    return c;
+}
+
 // LIFE_TAIL_SPLIT=0: no half-height tail tiles (A/B knob)
 static bool tail_split_enabled() {
     static const bool on = [] {
@@ -1745,6 +1775,7 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
         }
     }
     a.xcd_n = (bit ? xcd_order_enabled() : xcd_order_byte_enabled()) ? (a.half_first > 0 ? a.half_first : items) : 0;
+    a.strip = bit ? 0 : byte_strip();
     if (valu_lane_ops) {
         *valu_lane_ops = (double)(a.half_first > 0 ? a.half_first : items) * 64.0 * tstep_valu_per_tile_lane(m, !bit);
         if (a.half_first > 0)  // half tiles: R / 2 register rows per wave

@@ -355,7 +355,7 @@ def test_onegen_tunings(gpu, oracle, kernel):
                     assert life.last_path() == "onegen"
                     np.testing.assert_array_equal(life.gather(), want, err_msg=f"rows={rows} depth={depth}")
     finally:
-        gpu.tune(64, 2, kernel="byte")  # the library defaults (life_kernels.hip Tunings)
+        gpu.tune(16, 8, kernel="byte")  # the library defaults (life_kernels.hip Tunings)
         gpu.tune(16, 18, kernel="bit")
 
 
