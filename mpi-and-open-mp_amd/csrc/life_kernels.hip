@@ -302,9 +302,6 @@ struct TArgs {
     // [half_y, half_yend), half_ntx per tile row, so the last round of a
     // launch is made of half-length items (launch_tstep)
     int64_t half_first, half_y, half_ntx, half_yend;
-    // byte tiles: > 0 walks each region in strips of this many tile columns
-    // (LIFE_BYTE_STRIP)
-    int64_t strip;
     // XCD-aware order (bit, LIFE_XCD_ORDER): workgroups [0, xcd_n) are
     // renumbered so that each XCD (blocks b, b + 8, ... share one) walks a
     // contiguous row-major run of items; 0: dispatch order
@@ -658,22 +655,7 @@ __global__ __launch_bounds__(64 * NW, 4) void tstep_byte_kernel(TArgs a) {
     while (k + 1 < a.nreg && wg >= a.first[k + 1]) ++k;
     const int64_t wr = wg - a.first[k];
     const int64_t ntx = a.tx1[k] - a.tx0[k];
-    int64_t tx = a.tx0[k] + wr % ntx, ty = a.ty0[k] + wr / ntx;
-    if (a.strip > 0 && a.strip < ntx) {
-        // strip-major order: strips of `strip` tile columns walked down the
-        // region, so an XCD's run of items is a few columns wide and the tile
-        // below each tile (its 2K shared ghost rows) is in flight beside it
-        const int64_t C = a.strip, nty = a.ty1[k] - a.ty0[k], nfs = ntx / C, per = C * nty;
-        if (wr < nfs * per) {
-            const int64_t sI = wr / per, r = wr - sI * per;
-            ty = a.ty0[k] + r / C;
-            tx = a.tx0[k] + sI * C + r % C;
-        } else {
-            const int64_t r = wr - nfs * per, Cl = ntx - nfs * C;
-            ty = a.ty0[k] + r / Cl;
-            tx = a.tx0[k] + nfs * C + r % Cl;
-        }
-    }
+    const int64_t tx = a.tx0[k] + wr % ntx, ty = a.ty0[k] + wr / ntx;
     tile_body_byte<R, GK, WRAPX, WRAPY, NW>(a, a.in, a.out, tx, ty, xch);
 }
 
@@ -1655,23 +1637,17 @@ static bool xcd_order_enabled() {
 }
 // LIFE_XCD_ORDER_BYTE=0: dispatch order for the byte tiles.  The per-XCD
 // order measured (profiles/r03/r5b, 65536^2): 64.4-65.7 -> 66.9-67.0 T,
-// FETCH_SIZE x2 5.81 -> 5.41 GB per 32-generation launch, WRITE unchanged
+// FETCH_SIZE x2 5.81 -> 5.41 GB per 32-generation launch, WRITE unchanged.
+// Walking each XCD's run in strips of 4 / 8 / 16 tile columns instead (so the
+// tile below, sharing 64 ghost rows, is in flight beside each tile) fetched
+// 1-3 % less and ran 12 / 5 / 0 % slower (r5l): a 768 KB window per tile
+// leaves no L2 reuse to find
 static bool xcd_order_byte_enabled() {
     static const bool on = [] {
         const char *e = getenv("LIFE_XCD_ORDER_BYTE");
         return e ? atoi(e) != 0 : true;
     }();
     return on;
-}
-
-// LIFE_BYTE_STRIP=C: byte tiles walk strips of C tile columns (A/B knob; 0 = rows)
-static int64_t byte_strip() {
-    static const int64_t c = [] {
-        const char *e = getenv("LIFE_BYTE_STRIP");
-        const int v = e ? atoi(e) : 0;
-        return (int64_t)(v > 0 ? v : 0);
-    }();
-    return c;
 }
 
 // LIFE_TAIL_SPLIT=0: no half-height tail tiles (A/B knob)
@@ -1775,7 +1751,6 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
         }
     }
     a.xcd_n = (bit ? xcd_order_enabled() : xcd_order_byte_enabled()) ? (a.half_first > 0 ? a.half_first : items) : 0;
-    a.strip = bit ? 0 : byte_strip();
     if (valu_lane_ops) {
         *valu_lane_ops = (double)(a.half_first > 0 ? a.half_first : items) * 64.0 * tstep_valu_per_tile_lane(m, !bit);
         if (a.half_first > 0)  // half tiles: R / 2 register rows per wave
