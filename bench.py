@@ -94,6 +94,9 @@ def parse():
     p.add_argument("--flow", type=int, default=None, choices=[0, 1, 2],
                    help="LIFE_OPT_FLOW: single-shard bit tiles as one persistent dataflow launch per step call "
                         "(1 write-through, 2 fenced hand-off; 0 per-launch tiles; default: the library's)")
+    p.add_argument("--no-overlap", action="store_true",
+                   help="partitioned shards: every tile in one launch, then the halo exchange (LIFE_OPT_OVERLAP 0) "
+                        "instead of ring / interior / halo on three streams")
     p.add_argument("--loopback", action="store_true",
                    help="N = 1: run the single grid as a periodic partition of itself (LIFE_OPT_LOOPBACK): the "
                         "halo exchange, ring / interior overlap and (with --rank-mode) RCCL send/recv of the "
@@ -151,6 +154,8 @@ def make_life(a, nx, ny, dims, rank_mode, dist, rank, world, local_rank):
         life = lm.Life(nx, ny, shards=a.gpus, kernel=a.kernel, dims=dims)
     if a.flow is not None:
         life.configure(lm.OPT_FLOW, a.flow)
+    if a.no_overlap:
+        life.configure(lm.OPT_OVERLAP, 0)
     return life
 
 

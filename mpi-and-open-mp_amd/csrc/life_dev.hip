@@ -618,7 +618,10 @@ int generation_block(life_dev *d, int m) {
         auto launch = [&](const life::TileRegion *r, int n, bool timed, hipStream_t st) -> int {
             return launch_tiles(d, s, r, n, m, timed, st);
         };
-        if (!(rx || ry)) {
+        if (!(rx || ry) || !d->overlap) {
+            // one launch of every tile; a partitioned shard without overlap
+            // (LIFE_OPT_OVERLAP 0) then exchanges its halo on the compute
+            // stream, after the launch
             const life::TileRegion all{0, NX, 0, NY};
             CHK(launch(&all, 1, true, s.stream));
             continue;
@@ -648,6 +651,10 @@ int generation_block(life_dev *d, int m) {
     if (!(rx || ry)) {
         for (Shard &s : d->shards) s.cur ^= 1;
         return LIFE_OK;
+    }
+    if (!d->overlap) {
+        for (Shard &s : d->shards) s.cur ^= 1;
+        return exchange(d, 0, false);
     }
     CHK(exchange(d, 1, true));
     CHK(phase_end(d, pe));

@@ -48,11 +48,15 @@ def test_fill_random_matches_oracle(gpu, oracle, kernel, nx, ny, seed):
     (8, (4, 2), 4, 2), (4, (2, 2), 260, 260),
     (8, (1, 8), 64, 320), (4, (1, 4), 96, 132), (2, (1, 2), 300, 70),  # row strips (temporal)
 ])
-def test_multi_shard_local(gpu, oracle, kernel, shards, dims, nx, ny):
+@pytest.mark.parametrize("overlap", [True, False], ids=["overlap", "serial"])
+def test_multi_shard_local(gpu, oracle, kernel, shards, dims, nx, ny, overlap):
     """P logical shards on one GPU, halo through the LOCAL transport: the same
-    plan and pack/unpack kernels the RCCL transport runs."""
+    plan and pack/unpack kernels the RCCL transport runs; the overlapped
+    schedule (ring, interior and halo on three streams) and the serial one
+    (LIFE_OPT_OVERLAP 0: all tiles in one launch, then the halo)."""
     g0 = oracle.fill_random(nx, ny, seed=shards * 7 + nx, density=0.45)
-    with gpu.Life(nx, ny, shards=shards, kernel=kernel, dims=dims, transport=gpu.XPORT_LOCAL) as life:
+    with gpu.Life(nx, ny, shards=shards, kernel=kernel, dims=dims, transport=gpu.XPORT_LOCAL,
+                  overlap=overlap) as life:
         life.upload(g0)
         np.testing.assert_array_equal(life.gather(), g0)
         done = 0
