@@ -324,7 +324,7 @@ def main():
                         "kernel_avg_ms": round(avg_ms, 5), "kernel_launches": launches,
                         "generations_per_launch": round(gens_per_launch, 3), "ops_per_launch": valu_per_launch,
                         "model": "bit: per 64-cell pair row and generation 22 VALU (2 v_alignbit + 4 + 16 v_bitop3; "
-                                 "SQ_INSTS_VALU within 3.3 %, profiles/r03/r4h); byte: per 32-cell word row 12 + "
+                                 "SQ_INSTS_VALU 2.7 % above it, profiles/r03/r5p); byte: per 32-cell word row 12 + "
                                  "pack/unpack; life_kernels.hip tile_body_bit / tile_body_byte",
                         "hbm": hbm_obj}
         else:
