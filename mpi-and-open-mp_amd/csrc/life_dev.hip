@@ -143,17 +143,6 @@ static const int64_t kFlowMinPasses = [] {
     const int v = e ? atoi(e) : 0;
     return (int64_t)(v >= 2 ? v : 4);
 }();
-// CUs reserved for the halo stream of partitioned shards (LIFE_COMM_CUS,
-// shard_alloc); 0: none
-static int comm_cus() {
-    static const int v = [] {
-        const char *e = getenv("LIFE_COMM_CUS");
-        const int x = e ? atoi(e) : 0;
-        return x > 0 ? x : 0;
-    }();
-    return v;
-}
-
 // How timed stencil launches are bracketed (LIFE_TIMING_MODE, measurement
 // knob): 0 one event pair around a single-stream step call's launches (the
 // default: one hipEventRecord before the first launch, none between
@@ -214,28 +203,8 @@ int shard_alloc(life_dev *d, Shard &s) {
         HIPCHK(hipMemset(s.buf[i], 0, bytes));
     }
     HIPCHK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-    // Partitioned shards: the halo (pack, RCCL, unpack) waits for CU slots
-    // behind the interior launch that fills the chip -- its first RCCL kernel
-    // ran 284 us against 15 us alone on the one-GPU rehearsal
-    // (profiles/r03/r5r).  LIFE_COMM_CUS = r > 0 reserves r CUs (spread, one
-    // in every cus / r) for the comm stream and keeps the interior stream off
-    // them.
-    int cus = 0;
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s.device);
-    const int r = comm_cus();
-    if (r > 0 && cus > 2 * r) {
-        const int step = cus / r;
-        std::vector<uint32_t> inner((size_t)(cus + 31) / 32, 0u), comm((size_t)(cus + 31) / 32, 0u);
-        for (int i = 0; i < cus; i++) {
-            const bool reserved = i % step == step - 1 && i / step < r;
-            (reserved ? comm : inner)[(size_t)(i / 32)] |= 1u << (i % 32);
-        }
-        HIPCHK(hipExtStreamCreateWithCUMask(&s.stream2, (uint32_t)inner.size(), inner.data()));
-        HIPCHK(hipExtStreamCreateWithCUMask(&s.comm_stream, (uint32_t)comm.size(), comm.data()));
-    } else {
-        HIPCHK(hipStreamCreateWithFlags(&s.stream2, hipStreamNonBlocking));
-        HIPCHK(hipStreamCreateWithFlags(&s.comm_stream, hipStreamNonBlocking));
-    }
+    HIPCHK(hipStreamCreateWithFlags(&s.stream2, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&s.comm_stream, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&s.ev_int, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&s.ev_join, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&s.ev_ring, hipEventDisableTiming));
