@@ -16,11 +16,11 @@
 //
 //  * ByteEnc: 1 byte per cell.  SWAR on 4 cells per dword: horizontal sum via
 //    v_alignbyte, 9-cell sum n9 <= 9 per byte, rule ((n9 - c) | c) == 3.
-//  * BitEnc: 1 bit per cell, 32 cells per dword, x = bit 0 upward.
-//    Horizontal (L,C,R) full adder -> 2-bit sum per row; three rows add to
-//    n9 = u0 + 2*S; alive' = (n9 == 3) | (alive & n9 == 4).  Every boolean
-//    step is one v_bitop3_b32 (6 ops per row sum incl. 2 DPP moves, 8 for
-//    the rule).
+//  * BitEnc: 1 bit per cell in 64-cell interleaved pairs (E = even cells,
+//    O = odd cells, life_bitops.h).  Horizontal (L,C,R) full adder -> 2-bit
+//    sum per row; three rows add to n9 = u0 + 2*S; alive' = (n9 == 3) |
+//    (alive & n9 == 4).  Every boolean step is one v_bitop3_b32 (per pair:
+//    2 funnel shifts + 4 ops for the two rows sums, 2 x 8 for the rule).
 #include "life_kernels.h"
 #include "life_bitops.h"
 
