@@ -8,7 +8,10 @@
 //          bit-interleaved (E = even cells, O = odd cells): the right
 //          neighbour of an even cell is the odd word's same bit, so per PAIR
 //          of words 2 v_alignbit + 20 v_bitop3 and two neighbour fetches
-//          (pair_dpp: DPP + ds_bpermute; pair_bp: 2 ds_bpermute)
+//          (pair_dpp: DPP + ds_bpermute; pair_bp: 2 ds_bpermute; pair_1bp:
+//          1 ds_bpermute, the other neighbour the lane's own word; pair_nf: no
+//          fetch at all -- both neighbour words the lane's own: wrong cells,
+//          the same VALU, the LDS pipe's share of the loop)
 //
 // Every variant runs the same number of word-generations per lane; the
 // printed figure is ns per word-row-generation per SIMD (lower is better).
@@ -62,8 +65,9 @@ __global__ __launch_bounds__(512, 6) void k_word(uint32_t *out, uint32_t seed, i
     if (x == 0x12345678u) out[threadIdx.x] = x;
 }
 
-// BP: both neighbour words by ds_bpermute (else the left one by DPP)
-template <int R, bool BP>
+// F: 1 both neighbour words by ds_bpermute, 0 the left one by DPP, 2 neither
+// (own words), 3 the right one only
+template <int R, int F>
 __global__ __launch_bounds__(512, 6) void k_pair(uint32_t *out, uint32_t seed, int gens) {
     const int lane = threadIdx.x & 63;
     uint32_t e[R], o[R];
@@ -76,8 +80,8 @@ __global__ __launch_bounds__(512, 6) void k_pair(uint32_t *out, uint32_t seed, i
     for (int g = 0; g < gens; ++g) {
         // even cell 2i: O[i-1] + E[i] + O[i]; odd cell 2i+1: E[i] + O[i] + E[i+1]
         auto hsum = [&](uint32_t E, uint32_t O, uint32_t &e0, uint32_t &e1, uint32_t &o0, uint32_t &o1) {
-            const uint32_t en = bperm(raddr, E);
-            const uint32_t op = BP ? bperm(laddr, O) : left_or_zero(O);
+            const uint32_t en = (F == 0 || F == 1 || F == 3) ? bperm(raddr, E) : O;
+            const uint32_t op = F == 1 ? bperm(laddr, O) : F == 0 ? left_or_zero(O) : E;
             const uint32_t osh = __builtin_amdgcn_alignbit(O, op, 31);
             const uint32_t esh = __builtin_amdgcn_alignbit(en, E, 1);
             BitEnc::fa(osh, E, O, e0, e1);
@@ -119,9 +123,10 @@ int main() {
         kfn f;
         int words;  // words per lane and generation
     } ks[] = {{"word R48", k_word<48>, 48},          {"word R24", k_word<24>, 24},
-              {"pair_dpp R24", k_pair<24, false>, 48}, {"pair_bp R24", k_pair<24, true>, 48},
-              {"pair_dpp R16", k_pair<16, false>, 32}, {"pair_bp R16", k_pair<16, true>, 32},
-              {"pair_bp R32", k_pair<32, true>, 64}};
+              {"pair_dpp R24", k_pair<24, 0>, 48}, {"pair_bp R24", k_pair<24, 1>, 48},
+              {"pair_dpp R16", k_pair<16, 0>, 32}, {"pair_bp R16", k_pair<16, 1>, 32},
+              {"pair_bp R32", k_pair<32, 1>, 64}, {"pair_1bp R24", k_pair<24, 3>, 48},
+              {"pair_nf R24", k_pair<24, 2>, 48}, {"pair_bp R24 again", k_pair<24, 1>, 48}};
     const int gens = 200;
     for (const K &k : ks) {
         int per = 0;
