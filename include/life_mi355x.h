@@ -222,7 +222,11 @@ int life_dev_world(life_dev *d, int *world, int *dims0, int *dims1, int *nlocal,
  * bracketed by HIP events on the stream it runs on.  stats returns the mean
  * device time of one stencil launch (ms), the number of launches, and the
  * algorithmic HBM bytes one launch moves (1 B read + 1 B written per cell for
- * BYTE, 2 bits for BIT, over the cells that launch updates). */
+ * BYTE, 2 bits for BIT, over the cells that launch updates).  on = 1 also
+ * records the overlapped schedule's phase events (life_dev_phase_stats: ring,
+ * interior, halo, block); on = 2 times the launches only (their events are
+ * stamped by the dispatches themselves), leaving no event packets between the
+ * ring, halo and interior work of a partitioned step. */
 int life_dev_set_timing(life_dev *d, int on);
 
 /* Execution-path switches (defaults 1): LIFE_OPT_SMALL_GRID lets a

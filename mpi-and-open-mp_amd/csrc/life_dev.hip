@@ -163,6 +163,7 @@ struct life_dev {
     int transport = LIFE_XPORT_LOCAL;
     bool rank_mode = false;
     bool timing = false;
+    bool phase_events = true;  // timing on: also the overlapped schedule's phase events (life_dev_set_timing 1)
     bool overlap = true;
     int block_gens = 0;  // tiles: generations per launch at most (LIFE_OPT_BLOCK_GENS; default_block_gens)
     int small_mode = 1;  // grids that fit one CU: 0 off, 1 VGPR kernel else LDS kernel, 2 LDS kernel,
@@ -510,7 +511,10 @@ int launch_tiles(life_dev *d, Shard &s, const life::TileRegion *r, int nreg, int
     bool ev = false;
     if (d->timing && timed) CHK(launch_timer(d, s, 1, &t, &ev));
     double valu = 0.0;
-    const bool ext = ev && kEnvTimingMode == kTimeExt;  // events stamped by the dispatch itself
+    // events stamped by the dispatch itself: no event packets between the
+    // launches of a multi-stream step (kTimeCall's one pair per call is for
+    // single-stream calls)
+    const bool ext = ev && (kEnvTimingMode == kTimeExt || kEnvTimingMode == kTimeCall);
     if (ev && !ext) HIPCHK(hipEventRecord(t->a, st));
     HIPCHK(life::launch_tstep(s.lay, in, out, r, nreg, m, wrap_of(d), st, &valu, ext ? t->a : nullptr,
                               ext ? t->b : nullptr));
@@ -552,7 +556,7 @@ int join_streams(Shard &s) {
 // join on the compute stream.  Without timing: just the ring -> comm order.
 int phase_begin(life_dev *d, Shard &s, PhaseEvents **pe) {
     *pe = nullptr;
-    if (!d->timing) return LIFE_OK;
+    if (!d->timing || !d->phase_events) return LIFE_OK;
     int rc;
     *pe = phase_slot(s, &rc);
     if (!*pe) return rc;
@@ -1460,6 +1464,7 @@ int life_dev_set_timing(life_dev *d, int on) {
     d->ph_ring = d->ph_int = d->ph_halo = d->ph_block = 0.0;
     d->ph_blocks = 0;
     d->timing = on != 0;
+    d->phase_events = on != 2;
     d->acc_ms = 0.0;
     d->acc_launches = 0;
     d->acc_bytes = 0.0;

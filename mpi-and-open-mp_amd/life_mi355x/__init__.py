@@ -358,7 +358,9 @@ class Life:
         _check(_lib().life_dev_world(self._h, *[ctypes.byref(x) for x in v]), "world")
         return dict(zip(("world", "dims0", "dims1", "nlocal", "transport"), (x.value for x in v)))
 
-    def set_timing(self, on: bool) -> None:
+    def set_timing(self, on) -> None:
+        """life_dev_set_timing: False off, True launch timing + phase events,
+        2 launch timing only (no event packets inside a partitioned step)."""
         _check(_lib().life_dev_set_timing(self._h, int(on)), "set_timing")
 
     def last_path(self) -> str:

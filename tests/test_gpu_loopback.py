@@ -67,6 +67,30 @@ def test_loopback_no_overlap_and_toggle(gpu, oracle, kernel):
         np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, 74))
 
 
+@pytest.mark.parametrize("rccl", [None, "rank"], ids=["local", "rccl"])
+def test_loopback_timing_modes(gpu, oracle, rccl):
+    """set_timing(True) records the overlapped schedule's phase events,
+    set_timing(2) (bench.py's timed call) times the launches only: no phase
+    blocks, the tile launches still counted and timed, the same cells."""
+    nx, ny, gens = 16384, 1024, 64  # 4 x 3 interior tiles: the interior is its own launch
+    g0 = oracle.fill_random(nx, ny, seed=17, density=0.5)
+    with _make(gpu, nx, ny, "bit", rccl) as life:
+        life.upload(g0)
+        life.configure(gpu.OPT_LOOPBACK, 1)
+        life.set_timing(True)
+        life.step(24)
+        assert life.phase_stats()["blocks"] == 2  # 12 + 12
+        ms1, n1, _ = life.kernel_stats()
+        assert n1 == 2 and ms1 > 0  # the interior launches
+        life.set_timing(2)
+        life.step(gens - 24)
+        ph = life.phase_stats()
+        assert ph["blocks"] == 0 and ph["block_ms"] == 0.0
+        ms2, n2, _ = life.kernel_stats()
+        assert n2 == 4 and ms2 > 0  # 10 x 4 generations
+        np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, gens, threads=4))
+
+
 def test_loopback_rejected_for_partitioned(gpu):
     with gpu.Life(512, 512, shards=2, kernel="bit", transport=gpu.XPORT_LOCAL) as life:
         with pytest.raises(RuntimeError):
