@@ -248,8 +248,9 @@ def main():
     # "phases" object of an N > 1 line); the timed call times its launches
     # only, each stamped by its own dispatch, so that no event packets sit
     # between the ring, halo and interior work it measures (set_timing(2)).
-    # LIFE_BENCH_PHASES_TIMED=1: the phase events inside the timed call.
-    phases_timed = os.environ.get("LIFE_BENCH_PHASES_TIMED", "0") == "1"
+    # LIFE_BENCH_PHASES_TIMED=1 (or no warmup): the phase events inside the
+    # timed call.
+    phases_timed = os.environ.get("LIFE_BENCH_PHASES_TIMED", "0") == "1" or a.warmup <= 0
     life.set_timing(True)
     life.step(a.warmup)
     life.sync()

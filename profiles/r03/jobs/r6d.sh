@@ -8,7 +8,7 @@ O=gpurun_out/r6d
 rm -rf $O; mkdir -p $O
 S=scripts/gpu_step.sh
 R=$GRAFT_REPO_ROOT
-$S 500 $O/pytest.log python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_loopback.py tests/test_gpu_rank.py tests/test_gpu_bench.py -k "multi_shard or loopback or rank or bench" -x -q --timeout 250 --timeout-method thread -p no:cacheprovider || exit $?
+$S 500 $O/pytest.log python -u -m pytest tests/test_gpu_bench.py tests/test_gpu_parity.py tests/test_gpu_loopback.py tests/test_gpu_rank.py -k "multi_shard or loopback or rank or bench" -x -q --timeout 250 --timeout-method thread -p no:cacheprovider || exit $?
 tail -2 $O/pytest.log; grep -q " passed" $O/pytest.log && ! grep -q -E "[0-9]+ (failed|error)" $O/pytest.log || exit 1
 for i in 1 2; do
   for t in 1 0; do
