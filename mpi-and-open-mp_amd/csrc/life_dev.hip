@@ -149,6 +149,15 @@ static const int64_t kFlowMinPasses = [] {
 // launches), 1 per launch with hipEventRecord, 2 per launch stamped by the
 // dispatch itself (hipExtLaunchKernel), 3 no events.
 enum TimingMode { kTimeCall = 0, kTimeRecord = 1, kTimeExt = 2, kTimeOff = 3 };
+// LIFE_STREAM_PRIORITY (0/1, default 1): ring + comm streams at the greatest
+// HIP stream priority, the interior stream at the least (shard_alloc).
+static bool stream_priorities() {
+    static const bool v = [] {
+        const char *e = getenv("LIFE_STREAM_PRIORITY");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return v;
+}
 static const int kEnvTimingMode = [] {
     const char *e = getenv("LIFE_TIMING_MODE");
     const int v = e ? atoi(e) : 0;
@@ -195,17 +204,39 @@ bool part(const life_dev *d, int a) { return d->dims[a] > 1 || d->loop; }
 bool self_wrap_x(const life_dev *d) { return !d->loop && life::self_wrap_x(d->shards[0].lay, d->dims[0]); }
 life::Wrap wrap_of(const life_dev *d) { return life::Wrap{!part(d, 0) && !self_wrap_x(d), !part(d, 1)}; }
 
+// Allocation fill of every shard buffer (LIFE_POISON, read at each
+// life_dev_create*): unset / 0 = zeros (a dead grid, what the reference's
+// calloc gives); 1 = 0xA5 in both grid buffers (cells, aprons, pitch padding,
+// slack rows), the column staging and the sink -- not a dead cell in either
+// encoding, so a cell a kernel should have written but did not, or an apron
+// read before its halo arrived, changes the result on every run instead of
+// hiding behind a zeroed buffer that looks like a dead grid.
+int alloc_fill_byte() {
+    const char *e = getenv("LIFE_POISON");
+    return e && atoi(e) != 0 ? 0xA5 : 0;
+}
+
 int shard_alloc(life_dev *d, Shard &s) {
     HIPCHK(hipSetDevice(s.device));
+    // The streams first: every fill below is ordered on the stream that later
+    // uses the buffer (the null stream does not order against non-blocking
+    // streams), and finished before the shard is handed out.
+    // Priorities: the comm stream and the ring stream (the work the halo
+    // waits for) at the greatest priority, the interior at the least, so the
+    // halo kernels get CU slots ahead of queued interior tiles.
+    int prio_lo = 0, prio_hi = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    const bool prio = stream_priorities();
+    HIPCHK(hipStreamCreateWithPriority(&s.stream, hipStreamNonBlocking, prio ? prio_hi : 0));
+    HIPCHK(hipStreamCreateWithPriority(&s.stream2, hipStreamNonBlocking, prio ? prio_lo : 0));
+    HIPCHK(hipStreamCreateWithPriority(&s.comm_stream, hipStreamNonBlocking, prio ? prio_hi : 0));
+    const int fill = alloc_fill_byte();
     const int64_t slack = s.lay.generations_per_exchange > 1 ? life::kTemporalSlackRows : 0;
     const size_t bytes = (size_t)(s.lay.pitch * (s.lay.rows + slack));
     for (int i = 0; i < 2; i++) {
         HIPCHK(hipMalloc(&s.buf[i], bytes));
-        HIPCHK(hipMemset(s.buf[i], 0, bytes));
+        HIPCHK(hipMemsetAsync(s.buf[i], fill, bytes, s.stream));
     }
-    HIPCHK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&s.stream2, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&s.comm_stream, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&s.ev_int, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&s.ev_join, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&s.ev_ring, hipEventDisableTiming));
@@ -217,6 +248,11 @@ int shard_alloc(life_dev *d, Shard &s) {
     HIPCHK(hipMalloc(&s.col_recv, col_bytes));
     HIPCHK(hipMalloc(&s.d_count, 2 * sizeof(unsigned long long)));
     HIPCHK(hipMalloc(&s.sink, 1024));
+    HIPCHK(hipMemsetAsync(s.col_send, fill, col_bytes, s.stream));
+    HIPCHK(hipMemsetAsync(s.col_recv, fill, col_bytes, s.stream));
+    HIPCHK(hipMemsetAsync(s.d_count, 0, 2 * sizeof(unsigned long long), s.stream));
+    HIPCHK(hipMemsetAsync(s.sink, fill, 1024, s.stream));
+    HIPCHK(hipStreamSynchronize(s.stream));
     HIPCHK(hipHostMalloc(&s.h_count, 2 * sizeof *s.h_count, hipHostMallocDefault));
     life_halo_op ops[16];
     const int n = life::halo_plan(d->nx, d->ny, d->dims[0], d->dims[1], s.rank, d->kernel, d->loop, ops, 16);
@@ -722,10 +758,11 @@ double comm_timeout_s() {
 // hipStreamSynchronize with a deadline: polls the stream; on timeout aborts
 // the shard's communicator (which ends RCCL kernels stuck on a missing peer)
 // and fails with a message naming the operation.
-int bounded_sync(Shard &s, const char *what, int peer) {
+int bounded_sync(Shard &s, const char *what, int peer, hipStream_t st = nullptr) {
+    if (!st) st = s.stream;
     const auto t0 = std::chrono::steady_clock::now();
-    for (unsigned spin = 0;; ++spin) {
-        const hipError_t e = hipStreamQuery(s.stream);
+    for (;;) {
+        const hipError_t e = hipStreamQuery(st);
         if (e == hipSuccess) return LIFE_OK;
         if (e != hipErrorNotReady) {
             set_err("%s (peer %d): %s", what, peer, hipGetErrorString(e));
@@ -741,7 +778,9 @@ int bounded_sync(Shard &s, const char *what, int peer) {
                     s.rank, dt, peer);
             return LIFE_ERCCL;
         }
-        if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(spin > 4096 ? 1000 : 50));
+        // busy-poll the first 20 ms (a step's end is seen within a few us,
+        // as wait_stream), then back off to 1 ms naps
+        if (dt > 0.02) std::this_thread::sleep_for(std::chrono::microseconds(1000));
     }
 }
 
@@ -901,11 +940,13 @@ int life_dev_upload(life_dev *d, const uint8_t *grid) {
         HIPCHK(hipSetDevice(s.device));
         uint8_t *stage = nullptr;
         HIPCHK(hipMalloc(&stage, (size_t)(L.w * L.h)));
-        // Host buffers are the caller's pageable memory: blocking copies only
-        // (an async copy from/to pageable memory is staged by the runtime and
-        // was seen to race with the caller reading the buffer).
-        HIPCHK(hipMemcpy2D(stage, (size_t)L.w, grid + L.y0 * d->nx + L.x0, (size_t)d->nx, (size_t)L.w,
-                           (size_t)L.h, hipMemcpyHostToDevice));
+        // `grid` is the caller's pageable memory: the copy is ordered on the
+        // shard's stream (not the null stream, which does not order against
+        // the non-blocking shard streams) and waited for before this call
+        // returns, so the caller may reuse `grid` at once.
+        HIPCHK(hipMemcpy2DAsync(stage, (size_t)L.w, grid + L.y0 * d->nx + L.x0, (size_t)d->nx, (size_t)L.w,
+                                (size_t)L.h, hipMemcpyHostToDevice, s.stream));
+        HIPCHK(hipStreamSynchronize(s.stream));
         HIPCHK(life::launch_import_block(L, stage, s.buf[s.cur], s.stream));
         HIPCHK(hipStreamSynchronize(s.stream));
         HIPCHK(hipFree(stage));
@@ -1015,7 +1056,7 @@ static int step_flow(life_dev *d, int64_t generations, int64_t *done) {
         s.flow = nullptr;
         s.flow_words = 0;
         if (hipSetDevice(s.device) != hipSuccess || hipMalloc(&s.flow, words * sizeof(unsigned int)) != hipSuccess ||
-            hipMemset(s.flow, 0, 2 * sizeof(unsigned int)) != hipSuccess) {
+            hipMemsetAsync(s.flow, 0, 2 * sizeof(unsigned int), s.stream) != hipSuccess) {
             set_err("dataflow scratch (%zu words)", words);
             return LIFE_ENOMEM;
         }
@@ -1083,7 +1124,12 @@ int life_dev_step(life_dev *d, int64_t generations) {
         rc = step_body(d, generations);
         TimedLaunch *t = d->call_timer;
         d->call_timer = nullptr;
-        if (rc != LIFE_OK) return rc;
+        if (rc != LIFE_OK) {
+            // drop the half-recorded pair (no event b): a later harvest
+            // would fail on it and hide this call's error
+            s.timers_used--;
+            return rc;
+        }
         HIPCHK(hipEventRecord(t->b, s.stream));
         return LIFE_OK;
     }
@@ -1159,17 +1205,27 @@ int life_dev_sync(life_dev *d) {
     if (!d) return LIFE_EINVAL;
     for (Shard &s : d->shards) {
         HIPCHK(hipSetDevice(s.device));
-        HIPCHK(wait_stream(s.stream));
-        HIPCHK(wait_stream(s.stream2));
-        HIPCHK(wait_stream(s.comm_stream));
+        if (d->rank_mode && s.comm) {
+            // a step's halo waits on RCCL peers: a peer that died must not
+            // hang this rank (LIFE_COMM_TIMEOUT_S, then ncclCommAbort)
+            CHK(bounded_sync(s, "sync: compute stream", -1, s.stream));
+            CHK(bounded_sync(s, "sync: interior stream", -1, s.stream2));
+            CHK(bounded_sync(s, "sync: halo stream", -1, s.comm_stream));
+        } else {
+            HIPCHK(wait_stream(s.stream));
+            HIPCHK(wait_stream(s.stream2));
+            HIPCHK(wait_stream(s.comm_stream));
+        }
         if (s.flow_used) {
             // a dataflow launch whose dependency wait timed out (a broken
             // hand-off): its result cannot be trusted
             unsigned int err = 0;
-            HIPCHK(hipMemcpy(&err, s.flow + 1, sizeof err, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpyAsync(&err, s.flow + 1, sizeof err, hipMemcpyDeviceToHost, s.stream));
+            HIPCHK(hipStreamSynchronize(s.stream));
             s.flow_used = false;
             if (err) {
-                HIPCHK(hipMemset(s.flow + 1, 0, sizeof err));
+                HIPCHK(hipMemsetAsync(s.flow + 1, 0, sizeof err, s.stream));
+                HIPCHK(hipStreamSynchronize(s.stream));
                 set_err("dataflow tiles: item %u waited too long for its neighbours (state is invalid)", err - 1);
                 return LIFE_ESTATE;
             }
@@ -1235,16 +1291,20 @@ int gather_impl(life_dev *d, uint8_t *out, Frame fmt) {
     // BITS: a byte holding cells of two blocks (a block edge at x % 8 != 0)
     // is OR-ed together from both exports; those frame bytes start at 0
     std::vector<uint8_t> tmp;
-    auto place = [&](const life::GatherPiece &p, const uint8_t *src) -> int {
+    // `out` is the caller's pageable memory: each copy is ordered on the
+    // stream that produced `src` (never the null stream) and waited for.
+    auto place = [&](const life::GatherPiece &p, const uint8_t *src, hipStream_t st) -> int {
         const int64_t rb = p.row_bytes;
         uint8_t *dst = out + p.dst;
         if (!p.shared_first && !p.shared_last) {
-            // blocking: `out` is the caller's pageable memory
-            HIPCHK(hipMemcpy2D(dst, (size_t)frb, src, (size_t)rb, (size_t)rb, (size_t)p.rows, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy2DAsync(dst, (size_t)frb, src, (size_t)rb, (size_t)rb, (size_t)p.rows,
+                                    hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
             return LIFE_OK;
         }
         tmp.resize((size_t)p.bytes);
-        HIPCHK(hipMemcpy(tmp.data(), src, tmp.size(), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpyAsync(tmp.data(), src, tmp.size(), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
         const bool f = p.shared_first, l = p.shared_last;
         for (int64_t y = 0; y < p.rows; y++) {
             uint8_t *o = dst + y * frb;
@@ -1271,7 +1331,7 @@ int gather_impl(life_dev *d, uint8_t *out, Frame fmt) {
         for (Shard &s : d->shards) {  // every export is queued before the first copy waits
             HIPCHK(hipSetDevice(s.device));
             HIPCHK(hipStreamSynchronize(s.stream));
-            CHK(place(piece_of(s.rank), s.stage));
+            CHK(place(piece_of(s.rank), s.stage, s.stream));
         }
         return LIFE_OK;
     }
@@ -1290,10 +1350,10 @@ int gather_impl(life_dev *d, uint8_t *out, Frame fmt) {
     HIPCHK(hipStreamSynchronize(s.stream));
     // The root's own block sits in the front of the staging buffer; two
     // receive slots follow.  Block k+1 arrives over RCCL (non-blocking
-    // stream) while the host copies block k out of the other slot (a
-    // blocking copy into the caller's pageable memory), so the fan-in of
-    // world-1 blocks is not serialised behind the D2H copies.
-    CHK(place(plan[0], stage));  // copied out first: the buffer may grow below
+    // stream) while the host copies block k out of the other slot (on the
+    // idle second compute stream, into the caller's pageable memory), so the
+    // fan-in of world-1 blocks is not serialised behind the D2H copies.
+    CHK(place(plan[0], stage, s.stream));  // copied out first: the buffer may grow below
     CHK(stage_buffer(s, 2 * (size_t)slot, &stage));
     if (d->world > 1 && !s.comm) {
         set_err("gather: the root has no communicator");
@@ -1308,7 +1368,7 @@ int gather_impl(life_dev *d, uint8_t *out, Frame fmt) {
             NCCLCHK(ncclRecv(stage + (size_t)q.slot * (size_t)slot, (size_t)q.bytes, ncclUint8, q.rank, s.comm,
                              s.stream));
         }
-        CHK(place(p, stage + (size_t)p.slot * (size_t)slot));
+        CHK(place(p, stage + (size_t)p.slot * (size_t)slot, s.stream2));
     }
     HIPCHK(hipStreamSynchronize(s.stream));
     return LIFE_OK;

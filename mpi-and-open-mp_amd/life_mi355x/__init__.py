@@ -163,6 +163,18 @@ def _lib():
     return _LIB
 
 
+# Test hook: a byte value that fresh gather destinations are filled with
+# before the device copy (None: np.empty).  tests/conftest.py sets 0xA5, so a
+# copy that did not land shows up as poison instead of as a plausible grid.
+GATHER_FILL = None
+
+
+def _host_buffer(shape) -> np.ndarray:
+    if GATHER_FILL is None:
+        return np.empty(shape, dtype=np.uint8)
+    return np.full(shape, GATHER_FILL, dtype=np.uint8)
+
+
 def _check(rc: int, what: str) -> int:
     if rc < 0:
         raise LifeError(rc, what)
@@ -310,7 +322,7 @@ class Life:
 
     def gather(self, out: np.ndarray | None = None) -> np.ndarray:
         if out is None:
-            out = np.empty((self.ny, self.nx), dtype=np.uint8)
+            out = _host_buffer((self.ny, self.nx))
         _check(_lib().life_dev_gather(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))), "gather")
         return out
 
@@ -326,7 +338,7 @@ class Life:
         bit x & 7 of byte x >> 3; == np.packbits(gather(), axis=1,
         bitorder="little")), packed on the device."""
         if out is None:
-            out = np.empty((self.ny, (self.nx + 7) // 8), dtype=np.uint8)
+            out = _host_buffer((self.ny, (self.nx + 7) // 8))
         if out.shape != (self.ny, (self.nx + 7) // 8) or out.dtype != np.uint8 or not out.flags.c_contiguous:
             raise ValueError("gather_bits: out must be a C-contiguous uint8 (ny, ceil(nx/8)) array")
         _check(_lib().life_dev_gather_bits(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))), "gather_bits")

@@ -41,6 +41,9 @@ def lm():
     import life_mi355x
 
     life_mi355x._lib()
+    # gathers into fresh buffers see poison, not np.empty's leftovers, where
+    # the device copy did not land
+    life_mi355x.GATHER_FILL = 0xA5
     return life_mi355x
 
 

@@ -112,3 +112,60 @@ def test_rank0_times_out_when_a_rank_never_connects(harness):
                        capture_output=True, text=True, timeout=60)
     assert r.returncode == 1 and " rc -1 " in r.stdout, r.stdout
     assert 15 < time.monotonic() - t < 45
+
+
+def test_stranger_neither_gets_the_id_nor_a_slot(harness):
+    """a connection that does not present the job's token (here
+    one that sends garbage, one that sends nothing) is dropped without the
+    id, and the real rank is still served."""
+    import time
+
+    port = free_port()
+    p0 = subprocess.Popen([harness], env=clean_env(RANK=0, WORLD_SIZE=2, LIFE_BOOTSTRAP_PORT=port),
+                          stdout=subprocess.PIPE, text=True)
+    got = []
+    for payload in (b"GET / HTTP/1.0\r\n\r\n", None):
+        for _ in range(200):  # rank 0 may not be listening yet
+            try:
+                c = socket.create_connection(("127.0.0.1", port), timeout=5)
+                break
+            except OSError:
+                time.sleep(0.05)
+        with c:
+            if payload:
+                c.sendall(payload)
+            c.settimeout(5)
+            try:
+                got.append(c.recv(256))
+            except socket.timeout:
+                got.append(b"timeout")
+    assert all(g in (b"", b"timeout") or not g.startswith(b"LIFEUID1") for g in got), got
+    p1 = subprocess.Popen([harness], env=clean_env(RANK=1, WORLD_SIZE=2, LIFE_BOOTSTRAP_PORT=port),
+                          stdout=subprocess.PIPE, text=True)
+    outs = [p.communicate(timeout=60)[0] for p in (p0, p1)]
+    assert p0.returncode == 0 and p1.returncode == 0, outs
+    assert outs[0].split(" id ")[1] == outs[1].split(" id ")[1]
+
+
+def test_other_job_token_is_refused(harness):
+    """Two ranks whose job tokens differ (LIFE_BOOTSTRAP_TOKEN) do not pair:
+    rank 1 gets no id and both time out instead of RCCL joining the wrong job."""
+    port = free_port()
+    procs = [subprocess.Popen([harness], env=clean_env(RANK=r, WORLD_SIZE=2, LIFE_BOOTSTRAP_PORT=port,
+                                                         LIFE_BOOTSTRAP_TOKEN=f"job{r}"),
+                              stdout=subprocess.PIPE, text=True) for r in (1, 0)]
+    outs = [p.communicate(timeout=90)[0] for p in procs]
+    assert all(p.returncode == 1 for p in procs), outs
+
+
+def test_unreachable_rank0_is_bounded(harness):
+    """a non-zero rank whose MASTER_ADDR never answers gives up at
+    the timeout (non-blocking connect), not after the kernel's SYN retries."""
+    import time
+
+    t = time.monotonic()
+    r = subprocess.run([harness], env=clean_env(RANK=1, WORLD_SIZE=2, MASTER_ADDR="10.255.255.1",
+                                                MASTER_PORT=free_port()),
+                       capture_output=True, text=True, timeout=90)
+    assert r.returncode == 1 and " rc -1 " in r.stdout, r.stdout
+    assert time.monotonic() - t < 40
