@@ -285,7 +285,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return [float(x) for x in t]
 
-    elapsed = allmax([elapsed])[0]
+    call = life.call_stats()  # host enqueue / device span of the timed call
+    elapsed, host_enq, pass_enq, span = allmax([elapsed, call["host_enqueue_ms"], call["pass_enqueue_max_ms"],
+                                                call["device_span_ms"]])
     avg_ms, launches, bytes_per_launch = life.kernel_stats()
     updates_per_launch, valu_per_launch = life.kernel_work()
     if phases_timed:
@@ -362,6 +364,15 @@ def main():
                        "partition": partition + (" + loopback (the shard its own neighbour)" if a.loopback else ""), "kernel_path": path,
                        "generations_per_exchange": lay.generations_per_exchange, "live_cells_end": live},
             "roofline": roofline,
+            # the timed call, self-diagnosing: CPU time
+            # spent enqueueing it (whole call / longest pass), the device span
+            # from its first work's start to its last work's end, and what the
+            # bench clock saw outside that span (launch latency, host gaps, the
+            # sync's wake-up); max over ranks
+            "call": {"elapsed_ms": round(elapsed * 1e3, 4), "host_enqueue_ms": round(host_enq, 4),
+                     "pass_enqueue_max_ms": round(pass_enq, 4), "passes": call["passes"],
+                     "device_span_ms": round(span, 4),
+                     "outside_span_ms": round(elapsed * 1e3 - span, 4) if span > 0 else None},
         }
         if n_gpus > 1 or a.loopback:
             out["phases"] = {"ring_ms": round(ph["ring_ms"], 4), "interior_ms": round(ph["interior_ms"], 4),

@@ -314,6 +314,20 @@ int life_dev_kernel_work(life_dev *d, double *cell_updates_per_launch, double *v
  * fully hidden).  Zeros when no block was timed (unpartitioned grids). */
 int life_dev_phase_stats(life_dev *d, double *ring_ms, double *interior_ms, double *halo_ms, double *block_ms,
                          int64_t *blocks);
+/* Timing on: where the wall time of the LAST life_dev_step call went
+ * (measurement support; no reference counterpart -- life_cart.c times whole
+ * runs with MPI_Wtime).  host_enqueue_ms: CPU time spent inside the call
+ * (every launch, event, RCCL group and copy it enqueues; the call returns
+ * before the device finishes); pass_enqueue_max_ms: the longest single pass
+ * (one generation_block / one generation) of it; passes: its passes;
+ * device_span_ms: from the first piece of work of the call starting on the
+ * device to the last one ending, max over the local shards (HIP events at
+ * the call's two ends on the compute stream, where the call's streams are
+ * joined).  A caller that brackets the call plus a sync with its own clock
+ * sees elapsed - device_span = launch latency + host-side gaps + the sync's
+ * wake-up.  Zeros before the first timed call. */
+int life_dev_call_stats(life_dev *d, double *host_enqueue_ms, double *pass_enqueue_max_ms, int64_t *passes,
+                        double *device_span_ms);
 
 /* Stencil tuning for the whole process, per kernel family (-1: both): rows
  * each lane walks (16/32/64) and rows of loads kept in flight (2/4/8, or 18

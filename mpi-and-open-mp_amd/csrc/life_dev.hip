@@ -88,6 +88,9 @@ struct Shard {
     hipStream_t comm_stream = nullptr;
     hipEvent_t ev_ring = nullptr, ev_halo = nullptr, ev_sync = nullptr, ev_int = nullptr, ev_join = nullptr;
     hipEvent_t ev_entry = nullptr;  // life_dev_step entry fence (see there)
+    // device span of the last step call (timing on): own_a / own_b recorded at
+    // the call's two ends, or the kTimeCall pair borrowed (span_a / span_b)
+    hipEvent_t own_a = nullptr, own_b = nullptr, span_a = nullptr, span_b = nullptr;
     ncclComm_t comm = nullptr;
     uint8_t *col_send = nullptr, *col_recv = nullptr;  // 2*h bytes each
     unsigned long long *d_count = nullptr;  // census: live count, checksum
@@ -149,12 +152,16 @@ static const int64_t kFlowMinPasses = [] {
 // launches), 1 per launch with hipEventRecord, 2 per launch stamped by the
 // dispatch itself (hipExtLaunchKernel), 3 no events.
 enum TimingMode { kTimeCall = 0, kTimeRecord = 1, kTimeExt = 2, kTimeOff = 3 };
-// LIFE_STREAM_PRIORITY (0/1, default 1): ring + comm streams at the greatest
+// LIFE_STREAM_PRIORITY (0/1, default 0): ring + comm streams at the greatest
 // HIP stream priority, the interior stream at the least (shard_alloc).
+// Measured off (profiles/r04/a): the RCCL-loopback halo stays 0.23 ms beside
+// the interior either way (86.5-91.2 T with, 90.0-90.8 T without), and the
+// LOCAL 4-shard strong line drops 48.9 -> 34.4 T (its device copies on the
+// high-priority stream slow the interior 0.148 -> 0.281 ms).
 static bool stream_priorities() {
     static const bool v = [] {
         const char *e = getenv("LIFE_STREAM_PRIORITY");
-        return e ? atoi(e) != 0 : true;
+        return e ? atoi(e) != 0 : false;
     }();
     return v;
 }
@@ -193,6 +200,11 @@ struct life_dev {
     // overlapped blocks of partitioned shards: summed ms per phase (timing on)
     double ph_ring = 0.0, ph_int = 0.0, ph_halo = 0.0, ph_block = 0.0;
     int64_t ph_blocks = 0;
+    // the last step call (life_dev_call_stats): host time inside it, its
+    // passes and the longest one's host time, whether span events exist
+    double call_host_ms = 0.0, call_pass_max_ms = 0.0;
+    int64_t call_passes = 0;
+    bool call_spans = false;
 };
 
 namespace {
@@ -221,9 +233,8 @@ int shard_alloc(life_dev *d, Shard &s) {
     // The streams first: every fill below is ordered on the stream that later
     // uses the buffer (the null stream does not order against non-blocking
     // streams), and finished before the shard is handed out.
-    // Priorities: the comm stream and the ring stream (the work the halo
-    // waits for) at the greatest priority, the interior at the least, so the
-    // halo kernels get CU slots ahead of queued interior tiles.
+    // Priorities (LIFE_STREAM_PRIORITY=1, off by default): the comm and ring
+    // streams at the greatest priority, the interior at the least.
     int prio_lo = 0, prio_hi = 0;
     HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
     const bool prio = stream_priorities();
@@ -279,7 +290,7 @@ void shard_free(Shard &s) {
     if (s.flow) (void)hipFree(s.flow);
     if (s.d_count) (void)hipFree(s.d_count);
     if (s.h_count) (void)hipHostFree(s.h_count);
-    for (hipEvent_t e : {s.ev_ring, s.ev_halo, s.ev_sync, s.ev_int, s.ev_join, s.ev_entry})
+    for (hipEvent_t e : {s.ev_ring, s.ev_halo, s.ev_sync, s.ev_int, s.ev_join, s.ev_entry, s.own_a, s.own_b})
         if (e) (void)hipEventDestroy(e);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     if (s.stream2) (void)hipStreamDestroy(s.stream2);
@@ -519,7 +530,7 @@ int harvest_phases(life_dev *d) {
         HIPCHK(hipSetDevice(s.device));
         for (size_t i = 0; i < s.phases_used; i++) {
             const PhaseEvents &p = s.phases[i];
-            HIPCHK(hipEventSynchronize(p.end));
+            for (hipEvent_t e : {p.end, p.ring1, p.int1, p.halo1}) HIPCHK(hipEventSynchronize(e));
             float r = 0.f, n = 0.f, h = 0.f, b = 0.f;
             HIPCHK(hipEventElapsedTime(&r, p.ring0, p.ring1));
             HIPCHK(hipEventElapsedTime(&n, p.int0, p.int1));
@@ -610,8 +621,10 @@ int phase_end(life_dev *d, const std::vector<PhaseEvents *> &pe) {
     for (size_t si = 0; si < d->shards.size(); ++si) {
         Shard &s = d->shards[si];
         HIPCHK(hipSetDevice(s.device));
-        HIPCHK(hipEventRecord(s.ev_halo, s.comm_stream));
+        // halo1 before ev_halo: `end` (after the join on ev_halo) then
+        // implies halo1 has completed too
         if (pe[si]) HIPCHK(hipEventRecord(pe[si]->halo1, s.comm_stream));
+        HIPCHK(hipEventRecord(s.ev_halo, s.comm_stream));
         CHK(join_streams(s));
         if (pe[si]) HIPCHK(hipEventRecord(pe[si]->end, s.stream));
     }
@@ -1095,10 +1108,30 @@ static int step_flow(life_dev *d, int64_t generations, int64_t *done) {
 }
 
 static int step_body(life_dev *d, int64_t generations);
+static int step_call(life_dev *d, int64_t generations);
+
+static double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+static void note_pass(life_dev *d, std::chrono::steady_clock::time_point t0) {
+    const double ms = ms_since(t0);
+    d->call_passes++;
+    if (ms > d->call_pass_max_ms) d->call_pass_max_ms = ms;
+}
 
 int life_dev_step(life_dev *d, int64_t generations) {
     if (!d || generations < 0) return LIFE_EINVAL;
     if (generations == 0) return LIFE_OK;
+    const auto t0 = std::chrono::steady_clock::now();
+    d->call_passes = 0;
+    d->call_pass_max_ms = 0.0;
+    d->call_spans = false;
+    const int rc = step_call(d, generations);
+    d->call_host_ms = ms_since(t0);
+    return rc;
+}
+
+static int step_call(life_dev *d, int64_t generations) {
     // Entry fence: the second compute stream and the comm stream start after
     // everything already queued on the compute stream (an asynchronous
     // fill_random and its halo fill, a small-grid launch, a gather's export),
@@ -1131,9 +1164,30 @@ int life_dev_step(life_dev *d, int64_t generations) {
             return rc;
         }
         HIPCHK(hipEventRecord(t->b, s.stream));
+        s.span_a = t->a;  // the call's pair is its span
+        s.span_b = t->b;
+        d->call_spans = true;
         return LIFE_OK;
     }
-    return step_body(d, generations);
+    if (!d->timing) return step_body(d, generations);
+    // timing on, any other call: one event at each end of the call on every
+    // shard's compute stream (the entry fence above orders the other streams
+    // after the first; every schedule joins them back into it at the end)
+    for (Shard &s : d->shards) {
+        HIPCHK(hipSetDevice(s.device));
+        if (!s.own_a) HIPCHK(hipEventCreate(&s.own_a));
+        if (!s.own_b) HIPCHK(hipEventCreate(&s.own_b));
+        HIPCHK(hipEventRecord(s.own_a, s.stream));
+    }
+    CHK(step_body(d, generations));
+    for (Shard &s : d->shards) {
+        HIPCHK(hipSetDevice(s.device));
+        HIPCHK(hipEventRecord(s.own_b, s.stream));
+        s.span_a = s.own_a;
+        s.span_b = s.own_b;
+    }
+    d->call_spans = true;
+    return LIFE_OK;
 }
 
 // The launches of one step call (life_dev_step after its entry fence).
@@ -1153,13 +1207,19 @@ static int step_body(life_dev *d, int64_t generations) {
         d->last_path = done > 0 ? LIFE_PATH_FLOW : LIFE_PATH_TILES;
         for (int64_t g = done; g < generations;) {
             const int m = next_block(d, generations - g);
+            const auto t0 = std::chrono::steady_clock::now();
             CHK(generation_block(d, m));
+            note_pass(d, t0);
             g += m;
         }
         return LIFE_OK;
     }
     d->last_path = LIFE_PATH_ONEGEN;
-    for (int64_t g = 0; g < generations; g++) CHK(generation(d));
+    for (int64_t g = 0; g < generations; g++) {
+        const auto t0 = std::chrono::steady_clock::now();
+        CHK(generation(d));
+        note_pass(d, t0);
+    }
     return LIFE_OK;
 }
 
@@ -1543,6 +1603,25 @@ int life_dev_phase_stats(life_dev *d, double *ring_ms, double *interior_ms, doub
     if (halo_ms) *halo_ms = d->ph_halo / n;
     if (block_ms) *block_ms = d->ph_block / n;
     if (blocks) *blocks = d->ph_blocks;
+    return LIFE_OK;
+}
+
+int life_dev_call_stats(life_dev *d, double *host_enqueue_ms, double *pass_enqueue_max_ms, int64_t *passes,
+                        double *device_span_ms) {
+    if (!d) return LIFE_EINVAL;
+    double span = 0.0;
+    if (d->call_spans)
+        for (Shard &s : d->shards) {
+            HIPCHK(hipSetDevice(s.device));
+            HIPCHK(hipEventSynchronize(s.span_b));
+            float ms = 0.f;
+            HIPCHK(hipEventElapsedTime(&ms, s.span_a, s.span_b));
+            span = std::max(span, (double)ms);
+        }
+    if (host_enqueue_ms) *host_enqueue_ms = d->call_host_ms;
+    if (pass_enqueue_max_ms) *pass_enqueue_max_ms = d->call_pass_max_ms;
+    if (passes) *passes = d->call_passes;
+    if (device_span_ms) *device_span_ms = span;
     return LIFE_OK;
 }
 

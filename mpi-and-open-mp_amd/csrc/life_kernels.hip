@@ -345,6 +345,19 @@ using XchP = uint32_t[2][NW + 2][8][64];
 // read beyond the tile, absorbed by the ghost lanes.  Only the loads and
 // stores differ (per-lane rows); the generation loop is the tile's.  gsh = 6:
 // an ordinary tile (nb = 1).
+// Timing-only experiment switches (scripts/build_variants.sh; results are
+// WRONG with either set, the parity tests do not apply): LIFE_EXP_NO_BARRIER
+// drops the per-generation workgroup barrier, LIFE_EXP_BPERM_SELF makes the
+// two neighbour fetches return the lane's own dwords (no LDS permute).
+// Together with SQ_WAIT_* they bound the barrier and the permute latency
+// separately.
+#ifndef LIFE_EXP_NO_BARRIER
+#define LIFE_EXP_NO_BARRIER 0
+#endif
+#ifndef LIFE_EXP_BPERM_SELF
+#define LIFE_EXP_BPERM_SELF 0
+#endif
+
 template <int R, bool WRAPX, bool WRAPY, int FLOW, int NW, bool BAND = false>
 __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in, uint8_t *out, int64_t tx,
                                               int64_t ty, XchP<NW> &xch, int gsh = 6, int nb = 1,
@@ -401,7 +414,10 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
         }
     }
     auto hsum = [&](uint32_t e, uint32_t o, uint32_t &e0, uint32_t &e1, uint32_t &o0, uint32_t &o1) {
-        BitEnc::pair_sums(e, o, bperm(laddr, o), bperm(raddr, e), e0, e1, o0, o1);
+        if (LIFE_EXP_BPERM_SELF)
+            BitEnc::pair_sums(e, o, o, e, e0, e1, o0, o1);
+        else
+            BitEnc::pair_sums(e, o, bperm(laddr, o), bperm(raddr, e), e0, e1, o0, o1);
     };
     // Register budget (80 VGPRs at 3 tiles per CU, R = 24: 48 hold the
     // window): only the rolling sums of three rows stay live across the
@@ -430,7 +446,7 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
         xch[par][wi + 1][1][lane] = pe1;
         xch[par][wi + 1][2][lane] = po0;
         xch[par][wi + 1][3][lane] = po1;
-        __syncthreads();
+        if (!LIFE_EXP_NO_BARRIER) __syncthreads();
         hsum(ve[1], vo[1], ce0, ce1, co0, co1);
         {
             // the wave above (slot 0 above the window: zero, dead ghost rows)

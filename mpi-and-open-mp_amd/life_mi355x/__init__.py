@@ -59,7 +59,7 @@ ABI_SYMBOLS = (
     "life_dev_layout", "life_dev_world", "life_dev_set_timing", "life_dev_kernel_stats",
     "life_tune", "life_tune_temporal", "life_dev_configure", "life_dev_kernel_work", "life_dev_checksum",
     "life_dev_gather_vtk", "life_dev_gather_bits", "life_dev_destroy", "life_measure_copy", "life_dev_phase_stats",
-    "life_dev_barrier", "life_device_count", "life_dev_last_path",
+    "life_dev_barrier", "life_device_count", "life_dev_last_path", "life_dev_call_stats",
 )
 PATHS = {0: "none", 1: "onegen", 2: "tiles", 3: "flow", 5: "small"}
 
@@ -154,6 +154,7 @@ def _lib():
         L.life_dev_kernel_stats.argtypes = [vp, P(ctypes.c_double), P(i64), P(ctypes.c_double)]
         L.life_dev_kernel_work.argtypes = [vp, P(ctypes.c_double), P(ctypes.c_double)]
         L.life_dev_phase_stats.argtypes = [vp] + [P(ctypes.c_double)] * 4 + [P(i64)]
+        L.life_dev_call_stats.argtypes = [vp, P(ctypes.c_double), P(ctypes.c_double), P(i64), P(ctypes.c_double)]
         L.life_tune.argtypes = [i32, i32, i32]
         L.life_tune_temporal.argtypes = [i32, i32]
         L.life_measure_copy.argtypes = [i32, i64, i32, P(ctypes.c_double)]
@@ -401,6 +402,17 @@ class Life:
         n = ctypes.c_int64()
         _check(_lib().life_dev_phase_stats(self._h, *[ctypes.byref(x) for x in v], ctypes.byref(n)), "phase_stats")
         return dict(zip(("ring_ms", "interior_ms", "halo_ms", "block_ms"), (x.value for x in v)), blocks=n.value)
+
+    def call_stats(self):
+        """Where the last step call's time went (life_dev_call_stats, timing
+        on): host enqueue ms (whole call, longest pass), passes, device span
+        ms (first work start to last work end, max over local shards)."""
+        h, pm, sp = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        n = ctypes.c_int64()
+        _check(_lib().life_dev_call_stats(self._h, ctypes.byref(h), ctypes.byref(pm), ctypes.byref(n),
+                                          ctypes.byref(sp)), "call_stats")
+        return {"host_enqueue_ms": h.value, "pass_enqueue_max_ms": pm.value, "passes": n.value,
+                "device_span_ms": sp.value}
 
     def close(self) -> None:
         if self._h:

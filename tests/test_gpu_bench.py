@@ -67,6 +67,9 @@ def test_weak_scaling_default_is_cartesian_8():
     assert (out["config"]["nx"], out["config"]["ny"]) == (262144, 131072)
     assert out["config"]["partition"] == "cart"
     assert out["parity_vs_1gpu"]["ok"] is True, out["parity_vs_1gpu"]
+    c = out["call"]  # the host enqueue cost of the 8-shard pass is in the line
+    assert c["passes"] == 4 and c["host_enqueue_ms"] >= c["pass_enqueue_max_ms"] > 0, c
+    assert 0 < c["device_span_ms"] <= c["elapsed_ms"], c
 
 
 def test_single_gpu_line_is_valu_roofline():
@@ -77,3 +80,5 @@ def test_single_gpu_line_is_valu_roofline():
     assert r["bound"] == "valu" and 0 < r["frac"] < 1 and r["unit"] == "Tlane-op/s"
     assert r["hbm"]["achieved"] > 0 and r["hbm"]["peak"] == 8000.0
     assert "parity_vs_1gpu" not in out and out["scaling"] == "weak"
+    c = out["call"]  # one event pair around the call's launches: span <= the bench clock
+    assert c["passes"] == 3 and 0 < c["device_span_ms"] <= c["elapsed_ms"] and c["host_enqueue_ms"] > 0, c
