@@ -284,6 +284,13 @@ int life_dev_set_timing(life_dev *d, int on);
  * persistent launches, each with passes x tiles + resident workgroups below
  * 2^31 pulls; a positive value caps the passes per launch further (tests). */
 #define LIFE_OPT_FLOW_CHUNK 8
+/* LIFE_OPT_DEEP_HALO (default 1; LIFE_DEEP_HALO=0 at load time turns it
+ * off): partitioned bit shards with K-deep aprons exchange their halo only
+ * when the next pass would outrun it -- the passes in between also advance
+ * the apron cells they will read (rows [-e, 0) and [h, h + e), the apron
+ * pairs), so one exchange feeds up to K generations instead of one pass of
+ * at most LIFE_OPT_BLOCK_GENS.  0: one exchange per pass.  Same results. */
+#define LIFE_OPT_DEEP_HALO 9
 int life_dev_configure(life_dev *d, int option, int value);
 /* The kernel family that ran the bulk of the last life_dev_step call:
  * LIFE_PATH_ONEGEN (one generation per launch), _TILES (temporally blocked

@@ -136,6 +136,12 @@ static const int kEnvFlow = [] {
     const int v = e ? atoi(e) : 0;
     return v >= 0 && v <= 2 ? v : 0;
 }();
+// LIFE_DEEP_HALO (0/1, default 1) sets LIFE_OPT_DEEP_HALO's default at load
+// time (generation_block).
+static const bool kEnvDeepHalo = [] {
+    const char *e = getenv("LIFE_DEEP_HALO");
+    return e ? atoi(e) != 0 : true;
+}();
 static int default_block_gens(int kernel) {
     return kEnvBlockGens ? kEnvBlockGens : (kernel == LIFE_KERNEL_BIT ? 12 : 32);
 }
@@ -187,6 +193,8 @@ struct life_dev {
     int win_rows = 0, win_halo = 0;  // windowed kernel: strip height R, halo rows K (0: automatic)
     bool loop = false;  // LIFE_OPT_LOOPBACK: the one shard exchanges both axes' halos with itself
     int last_path = LIFE_PATH_NONE;  // life_dev_last_path
+    bool deep = kEnvDeepHalo;  // LIFE_OPT_DEEP_HALO: one K-deep exchange feeds several passes
+    int since = 0;  // generations advanced since the aprons were last filled (deep halo)
     int flow = kEnvFlow;  // LIFE_OPT_FLOW: single-shard bit tiles as one persistent dataflow launch per
                           // step call (1: write-through hand-off, 2: plain stores + release; 0 off)
     int64_t flow_chunk = 0;  // LIFE_OPT_FLOW_CHUNK: passes per dataflow launch at most (0: automatic)
@@ -297,24 +305,43 @@ void shard_free(Shard &s) {
     if (s.comm_stream) (void)hipStreamDestroy(s.comm_stream);
 }
 
-// All local shards' `which` streams wait for each other (LOCAL transport).
-int local_barrier(life_dev *d, bool comm) {
-    for (Shard &s : d->shards) {
-        HIPCHK(hipSetDevice(s.device));
-        HIPCHK(hipEventRecord(s.ev_sync, comm ? s.comm_stream : s.stream));
-    }
-    for (Shard &s : d->shards) {
-        HIPCHK(hipSetDevice(s.device));
-        for (Shard &t : d->shards)
-            if (&t != &s) HIPCHK(hipStreamWaitEvent(comm ? s.comm_stream : s.stream, t.ev_sync, 0));
-    }
-    return LIFE_OK;
-}
-
 Shard *find_local(life_dev *d, int rank) {
     for (Shard &s : d->shards)
         if (s.rank == rank) return &s;
     return nullptr;
+}
+
+// LOCAL transport ordering around the copies of one halo phase, peers only
+// (an all-to-all barrier cost 8 x 7 stream waits per step of an 8-shard
+// pass: 1-2 ms of host time per pass, profiles/r04/b).  kind RECV (before the
+// copies): each shard's stream waits for the shards it receives from -- their
+// pack / previous phase is queued before their event.  kind SEND (after):
+// each shard waits for the shards that copy from it, so nothing it enqueues
+// next overwrites a message still being read.
+int local_order(life_dev *d, bool comm, int phase, int kind) {
+    auto st = [&](Shard &s) { return comm ? s.comm_stream : s.stream; };
+    for (Shard &s : d->shards) {
+        HIPCHK(hipSetDevice(s.device));
+        HIPCHK(hipEventRecord(s.ev_sync, st(s)));
+    }
+    for (Shard &s : d->shards) {
+        HIPCHK(hipSetDevice(s.device));
+        int seen[16], ns = 0;
+        for (const life_halo_op &o : s.plan) {
+            if (o.phase != phase || o.kind != kind || o.peer == s.rank) continue;
+            bool dup = false;
+            for (int i = 0; i < ns; i++) dup |= seen[i] == o.peer;
+            if (dup) continue;
+            seen[ns++] = o.peer;
+            Shard *t = find_local(d, o.peer);
+            if (!t) {
+                set_err("LOCAL transport: peer %d not in this process", o.peer);
+                return LIFE_ESTATE;
+            }
+            HIPCHK(hipStreamWaitEvent(st(s), t->ev_sync, 0));
+        }
+    }
+    return LIFE_OK;
 }
 
 // Pointer + size of the message of op `o` (the slot-th send or recv of its
@@ -372,7 +399,7 @@ int run_phase(life_dev *d, int phase, int which_rel, bool on_comm) {
         }
         NCCLCHK(ncclGroupEnd());
     } else {
-        CHK(local_barrier(d, on_comm));
+        CHK(local_order(d, on_comm, phase, LIFE_HALO_RECV));
         for (Shard &s : d->shards) {
             HIPCHK(hipSetDevice(s.device));
             int nr = 0;
@@ -419,7 +446,7 @@ int run_phase(life_dev *d, int phase, int which_rel, bool on_comm) {
                     HIPCHK(hipMemcpyPeerAsync(dp, s.device, sp, src->device, dn, stream_of(s)));
             }
         }
-        CHK(local_barrier(d, on_comm));
+        CHK(local_order(d, on_comm, phase, LIFE_HALO_SEND));
     }
     if (phase == 0)
         for (Shard &s : d->shards) {
@@ -430,9 +457,11 @@ int run_phase(life_dev *d, int phase, int which_rel, bool on_comm) {
 }
 
 // Halo of buffer `which_rel` (0 = cur, 1 = nxt) on the compute streams.
+// Every call fills the aprons K deep: the deep-halo count restarts.
 int exchange(life_dev *d, int which_rel, bool on_comm) {
     CHK(run_phase(d, 0, which_rel, on_comm));
     CHK(run_phase(d, 1, which_rel, on_comm));
+    d->since = 0;
     return LIFE_OK;
 }
 
@@ -551,7 +580,8 @@ bool temporal(const life_dev *d) { return d->shards[0].lay.generations_per_excha
 
 // Launches up to 4 tile regions of the temporal stencil as ONE kernel on
 // `st` (m generations, cur -> nxt), optionally timed.
-int launch_tiles(life_dev *d, Shard &s, const life::TileRegion *r, int nreg, int m, bool timed, hipStream_t st) {
+int launch_tiles(life_dev *d, Shard &s, const life::TileRegion *r, int nreg, int m, bool timed, hipStream_t st,
+                 life::Extend ext_ = life::Extend{}) {
     const uint8_t *in = s.buf[s.cur];
     uint8_t *out = s.buf[s.cur ^ 1];
     TimedLaunch *t = nullptr;
@@ -561,16 +591,19 @@ int launch_tiles(life_dev *d, Shard &s, const life::TileRegion *r, int nreg, int
     // events stamped by the dispatch itself: no event packets between the
     // launches of a multi-stream step (kTimeCall's one pair per call is for
     // single-stream calls)
+    const life::Extend xt = ext_;
     const bool ext = ev && (kEnvTimingMode == kTimeExt || kEnvTimingMode == kTimeCall);
     if (ev && !ext) HIPCHK(hipEventRecord(t->a, st));
     HIPCHK(life::launch_tstep(s.lay, in, out, r, nreg, m, wrap_of(d), st, &valu, ext ? t->a : nullptr,
-                              ext ? t->b : nullptr));
+                              ext ? t->b : nullptr, xt));
     if (ev && !ext) HIPCHK(hipEventRecord(t->b, st));
     if (d->timing && timed) {
-        const life::TileGeom g = life::tile_geom(s.lay, m);
+        const life::TileGeom g = life::tile_geom(life::extended_layout(s.lay, xt), m);
         for (int k = 0; k < nreg; k++) {
+            // owned cells only (a deep-halo pass's apron rows are not counted)
             const int64_t xa = r[k].tx0 * g.lanes * g.cells, xb = std::min(r[k].tx1 * g.lanes * g.cells, s.lay.w);
-            const int64_t ya = r[k].ty0 * g.rows, yb = std::min(r[k].ty1 * g.rows, s.lay.h);
+            const int64_t ya = std::max(r[k].ty0 * g.rows - xt.y, (int64_t)0),
+                          yb = std::min(r[k].ty1 * g.rows - xt.y, s.lay.h);
             if (xb > xa && yb > ya) {
                 // compulsory HBM bytes of the launch: each owned cell's bit is
                 // read once and written once per m-generation pass (0.25 B),
@@ -654,6 +687,31 @@ int next_block(const life_dev *d, int64_t remaining) {
 // copy.
 int generation_block(life_dev *d, int m) {
     const bool rx = part(d, 0) || self_wrap_x(d), ry = part(d, 1);
+    // Deep halo (bit tiles, partitioned axes, no self-wrapped x): the
+    // exchange of a K-deep halo is skipped while the aprons still hold the
+    // next pass's ghost cells -- this pass then also advances the apron cells
+    // the next one reads (life::Extend) -- and runs after the pass whose
+    // successor would outrun them.  A 20-generation call of two 10-generation
+    // passes exchanges once instead of twice (life_cart.c:73-74 exchanges
+    // every generation).
+    const int K = d->shards[0].lay.generations_per_exchange;
+    const bool deep = d->deep && (rx || ry) && !self_wrap_x(d) && d->kernel == LIFE_KERNEL_BIT && K > 1;
+    if (deep && d->since + m > K) CHK(exchange(d, 0, false));  // a longer pass than planned for
+    const int bmax = std::min(std::min(K, 32), d->block_gens > 0 ? d->block_gens : 32);
+    if (deep && d->since + m + bmax <= K) {
+        life::Extend xt;
+        xt.y = ry ? K - d->since - m : 0;
+        xt.x = part(d, 0);
+        for (Shard &s : d->shards) {
+            HIPCHK(hipSetDevice(s.device));
+            const life::TileGeom g = life::tile_geom(life::extended_layout(s.lay, xt), m);
+            const life::TileRegion all{0, g.ntx, 0, g.nty};
+            CHK(launch_tiles(d, s, &all, 1, m, true, s.stream, xt));
+        }
+        for (Shard &s : d->shards) s.cur ^= 1;
+        d->since += m;
+        return LIFE_OK;
+    }
     std::vector<PhaseEvents *> pe(d->shards.size(), nullptr);
     for (size_t si = 0; si < d->shards.size(); ++si) {
         Shard &s = d->shards[si];
@@ -1530,6 +1588,15 @@ int life_dev_configure(life_dev *d, int option, int value) {
     case LIFE_OPT_FLOW:
         if (value < 0 || value > 2) return LIFE_EINVAL;
         d->flow = value;
+        return LIFE_OK;
+    case LIFE_OPT_DEEP_HALO:
+        if (value < 0 || value > 1) return LIFE_EINVAL;
+        d->deep = value != 0;
+        // aprons that are valid only to the remaining depth: refill them
+        if (d->since > 0) {
+            CHK(exchange(d, 0, false));
+            return life_dev_sync(d);
+        }
         return LIFE_OK;
     case LIFE_OPT_FLOW_CHUNK:
         if (value < 0) return LIFE_EINVAL;

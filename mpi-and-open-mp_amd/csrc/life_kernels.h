@@ -90,11 +90,26 @@ int flow_slots(const life_layout &L);  // resident workgroups of L's dataflow ke
 hipError_t launch_tflow(const life_layout &L, const uint8_t *in, uint8_t *out, int m, int64_t passes,
                         unsigned int *head, unsigned int *done, Wrap wrap, int flow, hipStream_t s,
                         hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+// Deep-halo passes (bit tiles, partitioned axes): the pass also advances the
+// apron cells that stay valid for the next pass -- y rows [-y, 0) and
+// [h, h + y) (the tile grid then spans h + 2y rows from owned row -y; the
+// windows read at most y + m <= yapron rows above), and with x the apron
+// pairs -1 and W are stored by the tile lanes that hold them.  A K-deep halo
+// then feeds K generations (several passes) instead of one pass.
+struct Extend {
+    int64_t y = 0;
+    bool x = false;
+};
 // Up to 4 disjoint tile regions in one launch; *valu_lane_ops (optional):
 // the modelled VALU lane-ops of the launch as tiled (tstep_valu_per_tile_lane).
+// Regions are in tile coordinates of tile_geom(extended_layout(L, ext), m).
 hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, const TileRegion *r, int nreg,
                         int m, Wrap wrap, hipStream_t s,
-                        double *valu_lane_ops = nullptr, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+                        double *valu_lane_ops = nullptr, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr,
+                        Extend ext = Extend{});
+// The layout a deep-halo pass tiles: h + 2 ext.y rows starting ext.y rows
+// into the top apron.
+life_layout extended_layout(const life_layout &L, const Extend &ext);
 int temporal_rows(bool bit);      // register rows per wave: bit pair rows 16/24/32, byte word rows 32..96
 int tile_waves(bool bit);         // waves per tile workgroup: bit 8/12/16 (LIFE_TILE_WAVES), byte 8
 // VALU instructions the lanes at one lane position of a tile's waves issue

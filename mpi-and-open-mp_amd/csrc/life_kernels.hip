@@ -306,6 +306,9 @@ struct TArgs {
     // renumbered so that each XCD (blocks b, b + 8, ... share one) walks a
     // contiguous row-major run of items; 0: dispatch order
     int64_t xcd_n;
+    // deep-halo pass (Extend::x, bit): the lanes holding the apron pairs -1
+    // and W store them too
+    int32_t xext;
 };
 
 template <int NW>
@@ -489,8 +492,9 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
     // this wave's share of them (a half-height tile's ghost rows may span more
     // than one wave: K > R)
     const int r0 = min(max(K - wi * R, 0), R), r1 = min(max(NW * R - K - wi * R, 0), R);
-    const bool st = BAND ? (pin >= 1 && pin <= (1 << gsh) - 2 && j < a.W && gl < nb)
-                         : (lane >= 1 && lane <= 62 && j < a.W);
+    const bool st = (BAND ? (pin >= 1 && pin <= (1 << gsh) - 2 && j < a.W && gl < nb)
+                          : (lane >= 1 && lane <= 62 && j < a.W)) ||
+                    (a.xext && (!BAND || gl < nb) && (j == -1 || j == a.W));
     const int64_t yb = y0 + (BAND ? (int64_t)(gl < nb ? gl : 0) * T : 0);  // this lane's band
     const int64_t ylim = yend >= 0 ? yend : a.h;  // half tiles of a region stop at its last row
     uint8_t *q = out + (a.ya + yb + r0) * a.pitch + voff;
@@ -1702,15 +1706,28 @@ int64_t region_items(const TileGeom &g, const TileRegion &r) {
     return (r.tx1 - r.tx0 - 1) * (r.ty1 - r.ty0) + (r.ty1 - r.ty0 + B - 1) / B;
 }
 
-hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, const TileRegion *r, int nreg,
-                        int m, Wrap wrap, hipStream_t s, double *valu_lane_ops, hipEvent_t ev0, hipEvent_t ev1) {
-    const int K = L.generations_per_exchange;
-    const bool bit = is_bit(L);
+life_layout extended_layout(const life_layout &L, const Extend &ext) {
+    life_layout V = L;
+    V.h += 2 * ext.y;
+    V.yapron -= ext.y;
+    V.rows = V.h + 2 * V.yapron;
+    return V;
+}
+
+hipError_t launch_tstep(const life_layout &Lin, const uint8_t *in, uint8_t *out, const TileRegion *r, int nreg,
+                        int m, Wrap wrap, hipStream_t s, double *valu_lane_ops, hipEvent_t ev0, hipEvent_t ev1,
+                        Extend ext) {
+    const int K = Lin.generations_per_exchange;
+    const bool bit = is_bit(Lin);
     // m <= 32: the tile's edge lanes absorb at most 32 wrong cells; m <= the
-    // apron depth a partitioned axis provides
-    if (nreg < 0 || nreg > kMaxRegions || m > K || m > 32 || K < 2 || L.yapron != K ||
-        tile_waves(bit) * temporal_rows(bit) - 2 * tile_ghost(L, m) < 1 || (!bit && K != 16 && K != 32))
+    // apron depth a partitioned axis provides.  Deep-halo passes: bit only
+    // (the byte windows hold K ghost rows whatever m is), the window's top
+    // ghost rows inside the apron (y + m <= yapron), no wrapped axis extended.
+    if (nreg < 0 || nreg > kMaxRegions || m > K || m > 32 || K < 2 || Lin.yapron != K || ext.y < 0 ||
+        ((ext.y > 0 || ext.x) && (!bit || ext.y + m > K || (ext.y > 0 && wrap.y) || (ext.x && wrap.x))) ||
+        tile_waves(bit) * temporal_rows(bit) - 2 * tile_ghost(Lin, m) < 1 || (!bit && K != 16 && K != 32))
         return hipErrorInvalidValue;
+    const life_layout L = extended_layout(Lin, ext);
     const TileGeom g = tile_geom(L, m);
     TArgs a;
     a.in = in;
@@ -1721,6 +1738,7 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
     a.h = L.h;
     a.ya = L.yapron;
     a.m = m;
+    a.xext = ext.x ? 1 : 0;
     a.nreg = 0;
     a.first[0] = 0;
     a.gsh = (int32_t)g.gsh;

@@ -383,3 +383,64 @@ def test_wide_periodic_tile_columns(gpu, oracle, pairs, ny, gens, m):
         life.step(gens)
         assert life.last_path() == "tiles"
         np.testing.assert_array_equal(life.gather(), want)
+
+
+# ---------------------------------------------------------------- deep halo (bit, partitioned)
+@pytest.mark.parametrize("nx,ny,shards,dims", [
+    (512, 300, 4, (2, 2)), (640, 96, 2, (2, 1)), (256, 200, 2, (1, 2)), (1000, 70, 4, (2, 2)),
+    (4100, 150, 2, (2, 1)), (2000, 333, 6, (3, 2)), (130, 64, 2, (2, 1)), (64 * 63 * 2, 90, 2, (2, 1))])
+@pytest.mark.parametrize("overlap", [True, False], ids=["overlap", "serial"])
+def test_deep_halo(gpu, oracle, nx, ny, shards, dims, overlap):
+    """LIFE_OPT_DEEP_HALO: one K-deep exchange feeds several passes, the
+    passes in between also advance the apron rows / pairs they will read.
+    Call patterns that run 1, 2 and 3 passes between exchanges, a pass longer
+    than planned (LIFE_OPT_BLOCK_GENS raised mid-run: the exchange is forced
+    first), deep off mid-run (the aprons are refilled) -- x-only, y-only and
+    2-D partitions, widths with a partial last pair, a 64 * 63-pair block
+    (banded / full last tile column) -- against the oracle and against the
+    same run with one exchange per pass."""
+    g0 = oracle.fill_random(nx, ny, seed=nx + ny + shards, density=0.45)
+    calls = [(5, None), (20, None), (7, None), (31, 32), (12, 12), (9, "off"), (33, None), (1, "on"), (24, None)]
+    got = {}
+    for deep in (1, 0):
+        with gpu.Life(nx, ny, shards=shards, kernel="bit", dims=dims, transport=gpu.XPORT_LOCAL,
+                      overlap=overlap) as life:
+            life.configure(gpu.OPT_DEEP_HALO, deep)
+            life.upload(g0)
+            done = 0
+            for gens, opt in calls:
+                if opt == "off":
+                    life.configure(gpu.OPT_DEEP_HALO, 0)
+                elif opt == "on":
+                    life.configure(gpu.OPT_DEEP_HALO, deep)
+                elif opt is not None:
+                    life.configure(gpu.OPT_BLOCK_GENS, opt)
+                life.step(gens)
+                done += gens
+                if deep:
+                    np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, done, threads=4),
+                                                  err_msg=f"after {done} generations")
+            got[deep] = life.gather()
+    np.testing.assert_array_equal(got[1], got[0])
+
+
+@pytest.mark.parametrize("rccl", [None, "rank"], ids=["local", "rccl"])
+def test_deep_halo_exchange_count(gpu, oracle, rccl):
+    """The exchange count the deep halo buys: on the loopback (the shard its
+    own neighbour, RCCL or LOCAL), a 5-generation call, then a 20-generation
+    call (2 passes of 10, the driver's shape) records ONE overlapped block --
+    one exchange for 25 generations -- where the per-pass schedule records 3."""
+    nx, ny = 4096, 1024
+    g0 = oracle.fill_random(nx, ny, seed=23, density=0.5)
+    for deep, blocks in ((1, 1), (0, 3)):
+        life = (gpu.Life.for_rank(nx, ny, 0, 1, gpu.unique_id(), 0, kernel="bit") if rccl
+                else gpu.Life(nx, ny, kernel="bit"))
+        with life:
+            life.upload(g0)
+            life.configure(gpu.OPT_LOOPBACK, 1)
+            life.configure(gpu.OPT_DEEP_HALO, deep)
+            life.set_timing(True)
+            life.step(5)
+            life.step(20)
+            assert life.phase_stats()["blocks"] == blocks
+            np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, 25, threads=4))
