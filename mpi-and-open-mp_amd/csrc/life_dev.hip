@@ -685,7 +685,13 @@ int next_block(const life_dev *d, int64_t remaining) {
 // (xa = the x-apron, one lane column).  A self-wrapped x axis
 // (life::self_wrap_x) counts as partitioned: its "exchange" is the column
 // copy.
-int generation_block(life_dev *d, int m) {
+// Deep halo applies (generation_block): bit tiles, a partitioned axis, no
+// self-wrapped x.
+bool deep_halo(const life_dev *d) {
+    return d->deep && d->kernel == LIFE_KERNEL_BIT && temporal(d) && (part(d, 0) || part(d, 1)) && !self_wrap_x(d);
+}
+
+int generation_block(life_dev *d, int m, bool last) {
     const bool rx = part(d, 0) || self_wrap_x(d), ry = part(d, 1);
     // Deep halo (bit tiles, partitioned axes, no self-wrapped x): the
     // exchange of a K-deep halo is skipped while the aprons still hold the
@@ -694,11 +700,14 @@ int generation_block(life_dev *d, int m) {
     // successor would outrun them.  A 20-generation call of two 10-generation
     // passes exchanges once instead of twice (life_cart.c:73-74 exchanges
     // every generation).
+    // step_body cuts a call into passes that end on the K boundary, so the
+    // exchange runs (overlapped with this pass) when the aprons are used up,
+    // or at the call's end when the next call's first pass could not fit.
     const int K = d->shards[0].lay.generations_per_exchange;
-    const bool deep = d->deep && (rx || ry) && !self_wrap_x(d) && d->kernel == LIFE_KERNEL_BIT && K > 1;
+    const bool deep = deep_halo(d);
     if (deep && d->since + m > K) CHK(exchange(d, 0, false));  // a longer pass than planned for
     const int bmax = std::min(std::min(K, 32), d->block_gens > 0 ? d->block_gens : 32);
-    if (deep && d->since + m + bmax <= K) {
+    if (deep && d->since + m < K && !(last && d->since + m + bmax > K)) {
         life::Extend xt;
         xt.y = ry ? K - d->since - m : 0;
         xt.x = part(d, 0);
@@ -1263,10 +1272,15 @@ static int step_body(life_dev *d, int64_t generations) {
         int64_t done = 0;
         CHK(step_flow(d, generations, &done));
         d->last_path = done > 0 ? LIFE_PATH_FLOW : LIFE_PATH_TILES;
+        const int K = d->shards[0].lay.generations_per_exchange;
         for (int64_t g = done; g < generations;) {
-            const int m = next_block(d, generations - g);
+            // deep halo: equal passes up to the next exchange boundary (32 =
+            // 11 + 11 + 10 at 12 generations per pass at most)
+            int64_t seg = generations - g;
+            if (deep_halo(d) && d->since < K) seg = std::min(seg, (int64_t)(K - d->since));
+            const int m = next_block(d, seg);
             const auto t0 = std::chrono::steady_clock::now();
-            CHK(generation_block(d, m));
+            CHK(generation_block(d, m, g + m >= generations));
             note_pass(d, t0);
             g += m;
         }
