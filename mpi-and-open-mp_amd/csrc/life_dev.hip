@@ -760,6 +760,11 @@ int generation_block(life_dev *d, int m, bool last) {
             if (ca > 0) ring[n++] = life::TileRegion{0, ca, ra, rb};
             if (cb < NX) ring[n++] = life::TileRegion{cb, NX, ra, rb};
         }
+        // the interior (second stream) starts after everything already on
+        // the compute stream: a deep-halo pass before this one is not joined
+        // into the other streams
+        HIPCHK(hipEventRecord(s.ev_entry, s.stream));
+        HIPCHK(hipStreamWaitEvent(s.stream2, s.ev_entry, 0));
         CHK(phase_begin(d, s, &pe[si]));
         CHK(launch(ring, n, false, s.stream));
         CHK(phase_ring(s, pe[si]));
