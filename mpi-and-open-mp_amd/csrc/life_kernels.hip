@@ -318,6 +318,22 @@ using Xch = uint32_t[2][NW][4][64];  // byte tiles: [parity][wave][top s0/s1, bo
 // wave index in the generation loop
 template <int NW>
 using XchP = uint32_t[2][NW + 2][8][64];
+// LIFE_BIT_REORDER (compile time, default 0): the generation loop publishes
+// its edge rows' sums, updates the interior rows, and only then meets the
+// barrier and updates rows 0 and R-1 -- the LDS writes drain while the
+// interior computes instead of right before the barrier.  Row 1's sums wait
+// in a wave-private LDS slot (XchB::priv; 8 KB per 8-wave tile) rather than
+// in 4 more VGPRs.
+#ifndef LIFE_BIT_REORDER
+#define LIFE_BIT_REORDER 0
+#endif
+template <int NW>
+struct XchB {
+    XchP<NW> s;
+#if LIFE_BIT_REORDER
+    uint32_t priv[NW][4][64];
+#endif
+};
 
 // Bit tiles over interleaved pairs.  Lane l of a tile holds pair column
 // 62 tx + l - 1 of R consecutive window rows as (E, O) register pairs; wave
@@ -363,8 +379,9 @@ using XchP = uint32_t[2][NW + 2][8][64];
 
 template <int R, bool WRAPX, bool WRAPY, int FLOW, int NW, bool BAND = false>
 __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in, uint8_t *out, int64_t tx,
-                                              int64_t ty, XchP<NW> &xch, int gsh = 6, int nb = 1,
+                                              int64_t ty, XchB<NW> &xb, int gsh = 6, int nb = 1,
                                               int64_t ybase = 0, int64_t yend = -1) {
+    XchP<NW> &xch = xb.s;
     static_assert(R >= 3, "window");
     const int K = a.m;  // ghost rows per window end
     const int T = NW * R - 2 * K;
@@ -433,6 +450,71 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
     // spilling (46-83 VGPRs at R = 24).
     if (wi == 0 || wi == NW - 1)  // the dead slots (ordered by the first barrier below)
         for (int q = 0; q < 16; ++q) xch[q >> 3][wi == 0 ? 0 : NW + 1][q & 7][lane] = 0u;
+#if LIFE_BIT_REORDER
+    for (int g = 0; g < a.m; ++g) {
+        const int par = g & 1;
+        uint32_t pe0, pe1, po0, po1, ce0, ce1, co0, co1;
+        {
+            uint32_t e0, e1, o0, o1;
+            hsum(ve[R - 1], vo[R - 1], e0, e1, o0, o1);
+            xch[par][wi + 1][4][lane] = e0;
+            xch[par][wi + 1][5][lane] = e1;
+            xch[par][wi + 1][6][lane] = o0;
+            xch[par][wi + 1][7][lane] = o1;
+        }
+        hsum(ve[0], vo[0], pe0, pe1, po0, po1);
+        xch[par][wi + 1][0][lane] = pe0;
+        xch[par][wi + 1][1][lane] = pe1;
+        xch[par][wi + 1][2][lane] = po0;
+        xch[par][wi + 1][3][lane] = po1;
+        hsum(ve[1], vo[1], ce0, ce1, co0, co1);
+        xb.priv[wi][0][lane] = ce0;
+        xb.priv[wi][1][lane] = ce1;
+        xb.priv[wi][2][lane] = co0;
+        xb.priv[wi][3][lane] = co1;
+#pragma unroll
+        for (int r = 1; r < R - 1; ++r) {
+            uint32_t ne0, ne1, no0, no1;
+            if (r + 1 == R - 1) {  // this wave's own bottom sums, published above
+                ne0 = xch[par][wi + 1][4][lane];
+                ne1 = xch[par][wi + 1][5][lane];
+                no0 = xch[par][wi + 1][6][lane];
+                no1 = xch[par][wi + 1][7][lane];
+            } else {
+                hsum(ve[r + 1], vo[r + 1], ne0, ne1, no0, no1);
+            }
+            ve[r] = BitEnc::rule1(pe0, pe1, ce0, ce1, ne0, ne1, ve[r]);
+            vo[r] = BitEnc::rule1(po0, po1, co0, co1, no0, no1, vo[r]);
+            pe0 = ce0;
+            pe1 = ce1;
+            po0 = co0;
+            po1 = co1;
+            ce0 = ne0;
+            ce1 = ne1;
+            co0 = no0;
+            co1 = no1;
+        }
+        if (!LIFE_EXP_NO_BARRIER) __syncthreads();
+        {
+            // row R-1: the old rows R-2 (p) and R-1 (c) and the wave below
+            const uint32_t de0 = xch[par][wi + 2][0][lane], de1 = xch[par][wi + 2][1][lane];
+            const uint32_t do0 = xch[par][wi + 2][2][lane], do1 = xch[par][wi + 2][3][lane];
+            ve[R - 1] = BitEnc::rule1(pe0, pe1, ce0, ce1, de0, de1, ve[R - 1]);
+            vo[R - 1] = BitEnc::rule1(po0, po1, co0, co1, do0, do1, vo[R - 1]);
+        }
+        {
+            // row 0: the wave above and this wave's old rows 0 and 1
+            const uint32_t ae0 = xch[par][wi][4][lane], ae1 = xch[par][wi][5][lane];
+            const uint32_t ao0 = xch[par][wi][6][lane], ao1 = xch[par][wi][7][lane];
+            const uint32_t te0 = xch[par][wi + 1][0][lane], te1 = xch[par][wi + 1][1][lane];
+            const uint32_t to0 = xch[par][wi + 1][2][lane], to1 = xch[par][wi + 1][3][lane];
+            const uint32_t se0 = xb.priv[wi][0][lane], se1 = xb.priv[wi][1][lane];
+            const uint32_t so0 = xb.priv[wi][2][lane], so1 = xb.priv[wi][3][lane];
+            ve[0] = BitEnc::rule1(ae0, ae1, te0, te1, se0, se1, ve[0]);
+            vo[0] = BitEnc::rule1(ao0, ao1, to0, to1, so0, so1, vo[0]);
+        }
+    }
+#else
     for (int g = 0; g < a.m; ++g) {
         const int par = g & 1;
         uint32_t pe0, pe1, po0, po1, ce0, ce1, co0, co1;
@@ -488,6 +570,7 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
             vo[R - 1] = BitEnc::rule1(po0, po1, co0, co1, do0, do1, vo[R - 1]);
         }
     }
+#endif
     // window rows [K, NW*R - K) are the tile's owned rows [ty*T, ty*T + T);
     // this wave's share of them (a half-height tile's ghost rows may span more
     // than one wave: K > R)
@@ -627,7 +710,7 @@ constexpr int bit_wpe(int NW, int R) { return NW == 16 ? (R <= 16 ? 8 : 4) : (R 
 // One workgroup per tile (or banded item / half-height tail tile).
 template <int R, bool WRAPX, bool WRAPY, int NW>
 __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tstep_bit_kernel(TArgs a) {
-    __shared__ XchP<NW> xch;
+    __shared__ XchB<NW> xch;
     int64_t wg = blockIdx.x;
     if (wg < a.xcd_n) {
         // the dispatcher deals blocks round-robin over the 8 XCDs: XCD x runs
@@ -708,7 +791,7 @@ struct FArgs {
 // base), more than they save.
 template <int R, bool WRAPX, bool WRAPY, int FLOW, int NW>
 __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tflow_kernel(FArgs f) {
-    __shared__ XchP<NW> xch;
+    __shared__ XchB<NW> xch;
     __shared__ unsigned int item_sh;
     const TArgs &a = f.t;
     const int64_t tiles = f.ntx * f.nty;

@@ -10,6 +10,13 @@ $S 900 $O/pytest.log python -u -m pytest tests -m gpu -x -q --timeout 120 --time
 grep -q " passed" $O/pytest.log && ! grep -q -E "[0-9]+ (failed|error)" $O/pytest.log || exit 1
 $S 120 $O/bench_driver.log python -u bench.py --steps 20 --warmup 5 || exit $?
 for i in 1 2; do
+  $S 120 $O/v_base_$i.log python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline || exit $?
+  LIFE_MI355X_LIB=$R/build_exp/reorder/liblife_mi355x.so $S 120 $O/v_reorder_$i.log python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline || exit $?
+  $S 120 $O/v_base992_$i.log python -u bench.py --no-cpu-baseline || exit $?
+  LIFE_MI355X_LIB=$R/build_exp/reorder/liblife_mi355x.so $S 120 $O/v_reorder992_$i.log python -u bench.py --no-cpu-baseline || exit $?
+done
+LIFE_MI355X_LIB=$R/build_exp/reorder/liblife_mi355x.so $S 300 $O/reorder_parity.log python -u -m pytest tests/test_gpu_parity.py -k "temporal_single_shard or wide_periodic or deep_halo" -x -q --timeout 120 --timeout-method thread -p no:cacheprovider || exit $?
+for i in 1 2; do
   for dh in 1 0; do
     LIFE_DEEP_HALO=$dh $S 200 $O/loop20_d${dh}_$i.log python -u bench.py --steps 20 --warmup 5 --rank-mode --loopback --no-cpu-baseline --no-parity || exit $?
     LIFE_DEEP_HALO=$dh $S 200 $O/loop992_d${dh}_$i.log python -u bench.py --rank-mode --loopback --no-cpu-baseline --no-parity || exit $?
