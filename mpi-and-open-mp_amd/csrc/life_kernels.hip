@@ -744,8 +744,14 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tstep_bit_kernel(TArg
     }
 }
 
+// Waves per SIMD the byte tiles are compiled for (LIFE_BYTE_WPE, compile
+// time, A/B): 4 = 2 tiles of 8 waves per CU (up to 128 VGPRs), 6 = 3 tiles
+// (80 VGPRs: the load / compute / store phases of three tiles overlap).
+#ifndef LIFE_BYTE_WPE
+#define LIFE_BYTE_WPE 4
+#endif
 template <int R, int GK, bool WRAPX, bool WRAPY, int NW>
-__global__ __launch_bounds__(64 * NW, 4) void tstep_byte_kernel(TArgs a) {
+__global__ __launch_bounds__(64 * NW, LIFE_BYTE_WPE) void tstep_byte_kernel(TArgs a) {
     __shared__ Xch<NW> xch;
     int64_t wg = blockIdx.x;
     if (wg < a.xcd_n) {  // per-XCD row-major runs, as tstep_bit_kernel
