@@ -335,16 +335,32 @@ def main():
                    if avg_ms > 0 else 0.0}
         tops = valu_per_launch / (avg_ms * 1e-3) / 1e12 if (valu_per_launch > 0 and avg_ms > 0) else 0.0
         if temporal and tops > 0:
-            # the temporally blocked kernels are bound by VALU issue, not HBM:
-            # modelled lane-ops per launch (checked against SQ_INSTS_VALU) over
-            # the same mean launch time, against 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
-            roofline = {"bound": "valu", "achieved": round(tops, 2), "peak": round(VALU_PEAK_TOPS, 2),
-                        "unit": "Tlane-op/s", "frac": round(tops / VALU_PEAK_TOPS, 4), "traffic": traffic,
+            # the temporally blocked kernels are bound by VALU issue, not HBM.
+            # achieved = ALGORITHMIC lane-ops per launch (the owned cells'
+            # updates x the op count of the formulation: bit 22 per 64-cell
+            # pair row and generation = 0.34375 per cell-update; byte 12 per
+            # 32-cell word row and generation + 35 per word row and launch for
+            # pack / unpack) over the mean launch time, against 256 CU x 4
+            # SIMD x 32 lanes x 2.4 GHz.  "issued" adds what the tiling spends
+            # on ghost rows and edge lanes (the kernel's op-count model as
+            # tiled; SQ_INSTS_VALU is 2.7 % above it, profiles/r03/r5p).
+            if a.kernel == "bit":
+                algo = updates_per_launch * 22.0 / 64.0
+            else:
+                cells = updates_per_launch / gens_per_launch if gens_per_launch > 0 else 0.0
+                algo = updates_per_launch * 12.0 / 32.0 + cells * 35.0 / 32.0
+            useful = algo / (avg_ms * 1e-3) / 1e12
+            roofline = {"bound": "valu", "achieved": round(useful, 2), "peak": round(VALU_PEAK_TOPS, 2),
+                        "unit": "Tlane-op/s", "frac": round(useful / VALU_PEAK_TOPS, 4), "traffic": traffic,
                         "kernel_avg_ms": round(avg_ms, 5), "kernel_launches": launches,
-                        "generations_per_launch": round(gens_per_launch, 3), "ops_per_launch": valu_per_launch,
-                        "model": "bit: per 64-cell pair row and generation 22 VALU (2 v_alignbit + 4 + 16 v_bitop3; "
-                                 "SQ_INSTS_VALU 2.7 % above it, profiles/r03/r5p); byte: per 32-cell word row 12 + "
-                                 "pack/unpack; life_kernels.hip tile_body_bit / tile_body_byte",
+                        "generations_per_launch": round(gens_per_launch, 3), "algorithmic_ops_per_launch": algo,
+                        "issued": {"achieved": round(tops, 2), "frac": round(tops / VALU_PEAK_TOPS, 4),
+                                   "ops_per_launch": valu_per_launch,
+                                   "note": "op-count model of the launch as tiled (ghost rows, edge lanes, "
+                                           "banded / half-height tiles included)"},
+                        "model": "bit: per 64-cell pair row and generation 22 VALU (2 v_alignbit + 4 + 16 v_bitop3); "
+                                 "byte: per 32-cell word row 12 per generation + 35 pack/unpack per launch; "
+                                 "life_kernels.hip tile_body_bit / tile_body_byte",
                         "hbm": hbm_obj}
         else:
             roofline = dict(hbm_obj, bound="hbm", traffic=traffic, kernel_avg_ms=round(avg_ms, 5),
