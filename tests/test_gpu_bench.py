@@ -81,7 +81,7 @@ def test_single_gpu_line_is_valu_roofline():
     # achieved = the algorithmic ops of the owned cells (22 per 64-cell pair row and generation); the issued
     # ops (ghost rows, edge lanes) are larger
     updates = r["algorithmic_ops_per_launch"] * 64.0 / 22.0
-    assert updates == pytest.approx(16384 * 16384 * r["generations_per_launch"], rel=1e-6)
+    assert updates == pytest.approx(16384 * 16384 * r["generations_per_launch"], rel=1e-3)  # rounded to 3 digits
     assert r["issued"]["ops_per_launch"] > r["algorithmic_ops_per_launch"] and r["issued"]["frac"] > r["frac"]
     assert r["hbm"]["achieved"] > 0 and r["hbm"]["peak"] == 8000.0
     assert "parity_vs_1gpu" not in out and out["scaling"] == "weak"
