@@ -155,7 +155,8 @@ def _lib():
         L.life_dev_kernel_stats.argtypes = [vp, P(ctypes.c_double), P(i64), P(ctypes.c_double)]
         L.life_dev_kernel_work.argtypes = [vp, P(ctypes.c_double), P(ctypes.c_double)]
         L.life_dev_phase_stats.argtypes = [vp] + [P(ctypes.c_double)] * 4 + [P(i64)]
-        L.life_dev_call_stats.argtypes = [vp, P(ctypes.c_double), P(ctypes.c_double), P(i64), P(ctypes.c_double)]
+        if hasattr(L, "life_dev_call_stats"):  # absent from pre-round-4 builds (LIFE_MI355X_LIB A/B runs)
+            L.life_dev_call_stats.argtypes = [vp, P(ctypes.c_double), P(ctypes.c_double), P(i64), P(ctypes.c_double)]
         L.life_tune.argtypes = [i32, i32, i32]
         L.life_tune_temporal.argtypes = [i32, i32]
         L.life_measure_copy.argtypes = [i32, i64, i32, P(ctypes.c_double)]
@@ -410,6 +411,8 @@ class Life:
         ms (first work start to last work end, max over local shards)."""
         h, pm, sp = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
         n = ctypes.c_int64()
+        if not hasattr(_lib(), "life_dev_call_stats"):
+            return {"host_enqueue_ms": 0.0, "pass_enqueue_max_ms": 0.0, "passes": 0, "device_span_ms": 0.0}
         _check(_lib().life_dev_call_stats(self._h, ctypes.byref(h), ctypes.byref(pm), ctypes.byref(n),
                                           ctypes.byref(sp)), "call_stats")
         return {"host_enqueue_ms": h.value, "pass_enqueue_max_ms": pm.value, "passes": n.value,
