@@ -400,6 +400,11 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
         jl = j > a.W ? a.W : j;  // pairs -1 .. W hold cells / apron; beyond: clamp (never stored)
     }
     const uint32_t voff = (uint32_t)(a.xoff + 8 * jl);
+    // this lane stores its pair column (decided here: one lane mask, not the
+    // 64-bit column index, lives across the generation loop)
+    const bool st = (BAND ? (pin >= 1 && pin <= (1 << gsh) - 2 && j < a.W && gl < nb)
+                          : (lane >= 1 && lane <= 62 && j < a.W)) ||
+                    (a.xext && (!BAND || gl < nb) && (j == -1 || j == a.W));
     const int64_t y0 = ybase + ty * T - K + (int64_t)wi * R;  // owned row of register row 0 (>= -K)
     // Row pointers are walked: with a periodic y axis the walk wraps at h;
     // with an apron the last tile's window may run past the apron row h+K-1
@@ -575,9 +580,6 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
     // this wave's share of them (a half-height tile's ghost rows may span more
     // than one wave: K > R)
     const int r0 = min(max(K - wi * R, 0), R), r1 = min(max(NW * R - K - wi * R, 0), R);
-    const bool st = (BAND ? (pin >= 1 && pin <= (1 << gsh) - 2 && j < a.W && gl < nb)
-                          : (lane >= 1 && lane <= 62 && j < a.W)) ||
-                    (a.xext && (!BAND || gl < nb) && (j == -1 || j == a.W));
     const int64_t yb = y0 + (BAND ? (int64_t)(gl < nb ? gl : 0) * T : 0);  // this lane's band
     const int64_t ylim = yend >= 0 ? yend : a.h;  // half tiles of a region stop at its last row
     uint8_t *q = out + (a.ya + yb + r0) * a.pitch + voff;
