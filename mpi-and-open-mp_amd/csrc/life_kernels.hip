@@ -597,6 +597,15 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
     }
 }
 
+// Waves per SIMD the byte tiles are compiled for (LIFE_BYTE_WPE, compile
+// time, A/B): 4 = 2 tiles of 8 waves per CU (up to 128 VGPRs), 6 = 3 tiles
+// (80 VGPRs: the load / compute / store phases of three tiles overlap).
+#ifndef LIFE_BYTE_WPE
+#define LIFE_BYTE_WPE 4
+#endif
+#ifndef LIFE_BYTE_LOAD_CHUNK
+#define LIFE_BYTE_LOAD_CHUNK 0
+#endif
 // Byte tiles: lane l of a tile holds word column 62 tx + l - 1 -- 32 byte
 // cells, packed into one register word per row by v_dot4_u32_u8 on load
 // (two 16-B loads) and unpacked on store -- in the drifting frame
@@ -635,6 +644,11 @@ __device__ __forceinline__ void tile_body_byte(const TArgs &a, const uint8_t *in
         const uint8_t *p = row0 + y * a.pitch;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
+            // LIFE_BYTE_LOAD_CHUNK rows of loads in flight at most: a
+            // scheduling fence after every chunk keeps the load phase's
+            // registers (8 per row in flight) inside the occupancy budget
+            if (LIFE_BYTE_LOAD_CHUNK > 0 && r > 0 && r % LIFE_BYTE_LOAD_CHUNK == 0)
+                __builtin_amdgcn_sched_barrier(0);
             const uint4 *q = reinterpret_cast<const uint4 *>(p + voff);
             v[r] = pack32(q[0], q[1]);
             ++y;
@@ -746,12 +760,6 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tstep_bit_kernel(TArg
     }
 }
 
-// Waves per SIMD the byte tiles are compiled for (LIFE_BYTE_WPE, compile
-// time, A/B): 4 = 2 tiles of 8 waves per CU (up to 128 VGPRs), 6 = 3 tiles
-// (80 VGPRs: the load / compute / store phases of three tiles overlap).
-#ifndef LIFE_BYTE_WPE
-#define LIFE_BYTE_WPE 4
-#endif
 template <int R, int GK, bool WRAPX, bool WRAPY, int NW>
 __global__ __launch_bounds__(64 * NW, LIFE_BYTE_WPE) void tstep_byte_kernel(TArgs a) {
     __shared__ Xch<NW> xch;
