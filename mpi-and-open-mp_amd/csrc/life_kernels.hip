@@ -370,6 +370,17 @@ struct XchB {
 // two neighbour fetches return the lane's own dwords (no LDS permute).
 // Together with SQ_WAIT_* they bound the barrier and the permute latency
 // separately.
+// LIFE_BIT_PAD (default 1): VGPRs kept live across the generation loop for
+// nothing but the register allocator's sake.  How many sources of the loop's
+// v_bitop3 fall into one VGPR bank (reg % 4) depends on the allocation, which
+// no source construct controls; three sources in one bank cost 2-3 % of the
+// launch (r4b: 11 such instructions per generation, 0.411-0.419 ms; the same
+// loop with 155: 0.419-0.431 ms on the same box, profiles/r04/g, h).  One
+// padding register gives 10 / 10 / 1 in the three loops (half-height, tile,
+// banded) of every instance; tests/test_isa.py pins the count.
+#ifndef LIFE_BIT_PAD
+#define LIFE_BIT_PAD 1
+#endif
 #ifndef LIFE_EXP_NO_BARRIER
 #define LIFE_EXP_NO_BARRIER 0
 #endif
@@ -400,11 +411,14 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
         jl = j > a.W ? a.W : j;  // pairs -1 .. W hold cells / apron; beyond: clamp (never stored)
     }
     const uint32_t voff = (uint32_t)(a.xoff + 8 * jl);
-    // this lane stores its pair column (decided here: one lane mask, not the
-    // 64-bit column index, lives across the generation loop)
-    const bool st = (BAND ? (pin >= 1 && pin <= (1 << gsh) - 2 && j < a.W && gl < nb)
-                          : (lane >= 1 && lane <= 62 && j < a.W)) ||
-                    (a.xext && (!BAND || gl < nb) && (j == -1 || j == a.W));
+#if LIFE_BIT_PAD > 0
+    uint32_t pad[LIFE_BIT_PAD];
+#pragma unroll
+    for (int i = 0; i < LIFE_BIT_PAD; ++i) {
+        pad[i] = voff + i;
+        asm volatile("" : "+v"(pad[i]));
+    }
+#endif
     const int64_t y0 = ybase + ty * T - K + (int64_t)wi * R;  // owned row of register row 0 (>= -K)
     // Row pointers are walked: with a periodic y axis the walk wraps at h;
     // with an apron the last tile's window may run past the apron row h+K-1
@@ -580,7 +594,26 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
     // this wave's share of them (a half-height tile's ghost rows may span more
     // than one wave: K > R)
     const int r0 = min(max(K - wi * R, 0), R), r1 = min(max(NW * R - K - wi * R, 0), R);
-    const int64_t yb = y0 + (BAND ? (int64_t)(gl < nb ? gl : 0) * T : 0);  // this lane's band
+    // Which lanes store, recomputed here from the lane id (the empty asm
+    // makes it a fresh value): nothing per-lane but voff and the window lives
+    // across the generation loop.  Extra live state there (the deep-halo
+    // apron-pair test kept the 64-bit column index alive) made the compiler
+    // issue each row's ds_bpermute right before its use and cost 2-8 % of the
+    // launch (tests/test_isa.py).  The apron pairs of a
+    // deep-halo pass (Extend::x) exist only on a partitioned x axis.
+    int lane2 = (int)(threadIdx.x & 63);
+    asm volatile("" : "+v"(lane2));
+#if LIFE_BIT_PAD > 0
+#pragma unroll
+    for (int i = 0; i < LIFE_BIT_PAD; ++i) asm volatile("" ::"v"(pad[i]));
+#endif
+    const int gl2 = BAND ? lane2 >> gsh : 0;
+    const int pin2 = BAND ? lane2 & ((1 << gsh) - 1) : lane2;
+    const int64_t j2 = tx * 62 + pin2 - 1;
+    const bool st = (BAND ? (pin2 >= 1 && pin2 <= (1 << gsh) - 2 && j2 < a.W && gl2 < nb)
+                          : (lane2 >= 1 && lane2 <= 62 && j2 < a.W)) ||
+                    (!WRAPX && a.xext && (!BAND || gl2 < nb) && (j2 == -1 || j2 == a.W));
+    const int64_t yb = y0 + (BAND ? (int64_t)(gl2 < nb ? gl2 : 0) * T : 0);  // this lane's band
     const int64_t ylim = yend >= 0 ? yend : a.h;  // half tiles of a region stop at its last row
     uint8_t *q = out + (a.ya + yb + r0) * a.pitch + voff;
 #pragma unroll
