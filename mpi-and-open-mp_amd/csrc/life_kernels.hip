@@ -370,17 +370,6 @@ struct XchB {
 // two neighbour fetches return the lane's own dwords (no LDS permute).
 // Together with SQ_WAIT_* they bound the barrier and the permute latency
 // separately.
-// LIFE_BIT_PAD (default 1): VGPRs kept live across the generation loop for
-// nothing but the register allocator's sake.  How many sources of the loop's
-// v_bitop3 fall into one VGPR bank (reg % 4) depends on the allocation, which
-// no source construct controls; three sources in one bank cost 2-3 % of the
-// launch (r4b: 11 such instructions per generation, 0.411-0.419 ms; the same
-// loop with 155: 0.419-0.431 ms on the same box, profiles/r04/g, h).  One
-// padding register gives 10 / 10 / 1 in the three loops (half-height, tile,
-// banded) of every instance; tests/test_isa.py pins the count.
-#ifndef LIFE_BIT_PAD
-#define LIFE_BIT_PAD 1
-#endif
 #ifndef LIFE_EXP_NO_BARRIER
 #define LIFE_EXP_NO_BARRIER 0
 #endif
@@ -411,14 +400,6 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
         jl = j > a.W ? a.W : j;  // pairs -1 .. W hold cells / apron; beyond: clamp (never stored)
     }
     const uint32_t voff = (uint32_t)(a.xoff + 8 * jl);
-#if LIFE_BIT_PAD > 0
-    uint32_t pad[LIFE_BIT_PAD];
-#pragma unroll
-    for (int i = 0; i < LIFE_BIT_PAD; ++i) {
-        pad[i] = voff + i;
-        asm volatile("" : "+v"(pad[i]));
-    }
-#endif
     const int64_t y0 = ybase + ty * T - K + (int64_t)wi * R;  // owned row of register row 0 (>= -K)
     // Row pointers are walked: with a periodic y axis the walk wraps at h;
     // with an apron the last tile's window may run past the apron row h+K-1
@@ -603,10 +584,6 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
     // deep-halo pass (Extend::x) exist only on a partitioned x axis.
     int lane2 = (int)(threadIdx.x & 63);
     asm volatile("" : "+v"(lane2));
-#if LIFE_BIT_PAD > 0
-#pragma unroll
-    for (int i = 0; i < LIFE_BIT_PAD; ++i) asm volatile("" ::"v"(pad[i]));
-#endif
     const int gl2 = BAND ? lane2 >> gsh : 0;
     const int pin2 = BAND ? lane2 & ((1 << gsh) - 1) : lane2;
     const int64_t j2 = tx * 62 + pin2 - 1;

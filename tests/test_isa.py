@@ -9,7 +9,9 @@ driver-shaped call on the same box (profiles/r04/e: 0.417-0.430 -> 0.450-0.461
 ms per launch).  These tests disassemble the built object and pin the
 schedule's shape, the VGPR budget (3 tiles per CU need <= 80) and the
 instruction counts DESIGN.md §5.1 models (22 VALU per pair row: 20 v_bitop3 +
-2 v_alignbit, 2 ds_bpermute).
+2 v_alignbit, 2 ds_bpermute).  (VGPR banks are not pinned: a build with 155
+v_bitop3 reading three sources from one bank ran as fast as one with 11,
+profiles/r04/i.)
 """
 import os
 import re
@@ -87,33 +89,6 @@ def test_bpermute_issued_ahead_of_use(isa):
             if o == "ds_bpermute_b32":
                 gaps.append(next(k for k in range(i, len(ops)) if ops[k] == "s_waitcnt") - i)
         assert sum(gaps) / len(gaps) >= 5.0, f"ds_bpermute -> s_waitcnt mean {sum(gaps) / len(gaps):.2f}"
-
-
-def test_vgpr_banks(isa):
-    """At most a handful of the loop's v_bitop3 / v_alignbit read all three
-    sources from one VGPR bank (reg % 4): 155 such instructions per
-    generation cost 2-3 % of the launch against 11 (profiles/r04/g, h)."""
-    for ops_text in generation_loop_texts(kernel_lines(isa[0])):
-        same = 0
-        for t in ops_text:
-            if t.startswith(("v_bitop3", "v_alignbit")):
-                regs = list(dict.fromkeys(int(x) for x in re.findall(r"\bv(\d+)\b", t)[1:]))
-                banks = {r % 4 for r in regs}
-                same += len(regs) == 3 and len(banks) == 1
-        assert same <= 40, f"{same} instructions with three sources in one VGPR bank"
-
-
-def generation_loop_texts(lines):
-    out = []
-    for addr, op, text in lines:
-        m = re.match(r"s_cbranch_\w+ (\d+)$", text)
-        if not m or int(m.group(1)) < 0x8000:
-            continue
-        target = addr + 4 + 4 * (int(m.group(1)) - 0x10000)
-        body = [t for a, _, t in lines if target <= a <= addr]
-        if any(t.startswith("s_barrier") for t in body) and len(body) > 300:
-            out.append(body)
-    return out
 
 
 def test_vgpr_budget(isa):
