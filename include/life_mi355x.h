@@ -291,6 +291,14 @@ int life_dev_set_timing(life_dev *d, int on);
  * pairs), so one exchange feeds up to K generations instead of one pass of
  * at most LIFE_OPT_BLOCK_GENS.  0: one exchange per pass.  Same results. */
 #define LIFE_OPT_DEEP_HALO 9
+/* LIFE_OPT_SKEW (default 0; LIFE_SKEW=1 at load time turns it on): a bit
+ * pass over a whole shard (every single-shard pass, the deep-halo passes of a
+ * partitioned one) runs as time-skewed parallelogram tiles -- each workgroup
+ * takes a segment of one tile column top to bottom, a tile's window drifts up
+ * one row per generation and takes the two rows above it from the tile
+ * before, so no ghost rows are recomputed (m <= 12 generations per launch;
+ * 24-row x 8-wave tiles).  Same results. */
+#define LIFE_OPT_SKEW 10
 int life_dev_configure(life_dev *d, int option, int value);
 /* The kernel family that ran the bulk of the last life_dev_step call:
  * LIFE_PATH_ONEGEN (one generation per launch), _TILES (temporally blocked

@@ -142,6 +142,11 @@ static const bool kEnvDeepHalo = [] {
     const char *e = getenv("LIFE_DEEP_HALO");
     return e ? atoi(e) != 0 : true;
 }();
+// LIFE_SKEW (0/1) sets LIFE_OPT_SKEW's default at load time.
+static const bool kEnvSkew = [] {
+    const char *e = getenv("LIFE_SKEW");
+    return e ? atoi(e) != 0 : false;
+}();
 static int default_block_gens(int kernel) {
     return kEnvBlockGens ? kEnvBlockGens : (kernel == LIFE_KERNEL_BIT ? 12 : 32);
 }
@@ -194,6 +199,7 @@ struct life_dev {
     bool loop = false;  // LIFE_OPT_LOOPBACK: the one shard exchanges both axes' halos with itself
     int last_path = LIFE_PATH_NONE;  // life_dev_last_path
     bool deep = kEnvDeepHalo;  // LIFE_OPT_DEEP_HALO: one K-deep exchange feeds several passes
+    bool skew = kEnvSkew;      // LIFE_OPT_SKEW: whole-shard bit passes as skewed (ghost-free) tiles
     int since = 0;  // generations advanced since the aprons were last filled (deep halo)
     int flow = kEnvFlow;  // LIFE_OPT_FLOW: single-shard bit tiles as one persistent dataflow launch per
                           // step call (1: write-through hand-off, 2: plain stores + release; 0 off)
@@ -594,8 +600,15 @@ int launch_tiles(life_dev *d, Shard &s, const life::TileRegion *r, int nreg, int
     const life::Extend xt = ext_;
     const bool ext = ev && (kEnvTimingMode == kTimeExt || kEnvTimingMode == kTimeCall);
     if (ev && !ext) HIPCHK(hipEventRecord(t->a, st));
-    HIPCHK(life::launch_tstep(s.lay, in, out, r, nreg, m, wrap_of(d), st, &valu, ext ? t->a : nullptr,
-                              ext ? t->b : nullptr, xt));
+    // the whole (extended) shard in one launch: the skewed tiles when enabled
+    const life::TileGeom gw = life::tile_geom(life::extended_layout(s.lay, xt), m);
+    const bool whole = nreg == 1 && r[0].tx0 == 0 && r[0].ty0 == 0 && r[0].tx1 >= gw.ntx && r[0].ty1 >= gw.nty;
+    if (d->skew && whole && life::skew_ok(s.lay, m))
+        HIPCHK(life::launch_tskew(s.lay, in, out, m, wrap_of(d), st, &valu, ext ? t->a : nullptr,
+                                  ext ? t->b : nullptr, xt));
+    else
+        HIPCHK(life::launch_tstep(s.lay, in, out, r, nreg, m, wrap_of(d), st, &valu, ext ? t->a : nullptr,
+                                  ext ? t->b : nullptr, xt));
     if (ev && !ext) HIPCHK(hipEventRecord(t->b, st));
     if (d->timing && timed) {
         const life::TileGeom g = life::tile_geom(life::extended_layout(s.lay, xt), m);
@@ -1607,6 +1620,10 @@ int life_dev_configure(life_dev *d, int option, int value) {
     case LIFE_OPT_FLOW:
         if (value < 0 || value > 2) return LIFE_EINVAL;
         d->flow = value;
+        return LIFE_OK;
+    case LIFE_OPT_SKEW:
+        if (value < 0 || value > 1) return LIFE_EINVAL;
+        d->skew = value != 0;
         return LIFE_OK;
     case LIFE_OPT_DEEP_HALO:
         if (value < 0 || value > 1) return LIFE_EINVAL;

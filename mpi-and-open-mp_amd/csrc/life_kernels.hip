@@ -770,6 +770,184 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tstep_bit_kernel(TArg
     }
 }
 
+// ------------------------------------------------------------------ skewed bit tiles
+// Parallelogram (time-skewed) tiles: no ghost rows.  A tile of NW waves x R
+// pair rows computes, at generation g, the domain rows [O + m - g, O + m - g
+// + NW*R): its window drifts up one row per generation, so every row's new
+// value reads the row itself and the two rows ABOVE it in register order
+// (new_i = rule(h(old_{i-2}), h(old_{i-1}), h(old_i), alive = old_{i-1})) and
+// nothing below.  The two rows above wave 0 come from the tile above at the
+// same generation, which the same workgroup ran just before (a segment of S
+// consecutive tiles of one tile column per workgroup, top to bottom), through
+// an LDS ring of one entry per generation; a segment's first tile takes them
+// from a 24-row prologue window (8 waves x 3 rows, its own top fed zeros:
+// the wrong values it starts with spread two rows per generation in window
+// terms and never reach its bottom two rows within m <= 12 generations).
+// After m generations register row i of wave w holds domain row O + wR + i:
+// tiles of 192 rows partition the domain, read it once (+ 24 prologue rows
+// per segment) and recompute nothing but the two rows above each wave (12
+// VALU per wave and generation, 2.3 %) -- where tile_body_bit recomputes 2m
+// ghost rows per 192-row window (10.4 % at m = 10).
+//
+// LDS: the inter-wave exchange holds the raw (E, O) of each wave's last two
+// rows per generation parity (16 KB at 8 waves), the ring the same four
+// dwords per generation for two tiles (tile parity: 24 KB): 40 KB, 3
+// workgroups per CU.
+struct KArgs {
+    const uint8_t *in;
+    uint8_t *out;
+    int64_t pitch, xoff, W, h, ya;  // domain: rows [0, h) start at buffer row ya; W pairs per row
+    int64_t ylo;                    // lowest readable domain row (non-wrapped y: -ya)
+    int64_t ntx, nty, seg, nsc;     // tile columns, tiles per column, tiles per segment, segments per column
+    int32_t m, xext;
+};
+template <int NW>
+struct XchS {
+    uint32_t x[2][NW][4][64];     // [gen parity][wave][E(R-2), O(R-2), E(R-1), O(R-1)][lane]
+    uint32_t ring[2][12][4][64];  // [tile parity][generation - 1][same][lane]
+    uint32_t sink[4][64];         // the other waves' copy of the ring write (no branch)
+};
+
+template <int R, bool WRAPX, bool WRAPY, int NW>
+__device__ __forceinline__ void tile_body_skew(const KArgs &a, int64_t tx, int64_t O, XchS<NW> &xs, int tpar,
+                                               bool prologue, bool first) {
+    static_assert(R >= 3, "window");
+    const int lane = threadIdx.x & 63;
+    const int laddr = ((lane - 1) & 63) << 2, raddr = ((lane + 1) & 63) << 2;
+    const int wi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int m = a.m;
+    const int64_t j = tx * 62 + lane - 1;  // pair column of this lane
+    int64_t jl;
+    if (WRAPX) {
+        jl = j % a.W;
+        if (jl < 0) jl += a.W;
+    } else {
+        jl = j > a.W ? a.W : j;
+    }
+    const uint32_t voff = (uint32_t)(a.xoff + 8 * jl);
+    // generation-0 domain row of register row 0 (the prologue: the NW*R rows
+    // above the tile's first input row)
+    const int64_t y0 = O + m + (int64_t)wi * R - (prologue ? (int64_t)NW * R : 0);
+    const uint8_t *row0 = a.in + a.ya * a.pitch;
+    uint32_t ve[R], vo[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        // one wave-uniform row per register row: wrapped, or clamped to the
+        // readable rows (only a prologue's top reaches above them, and those
+        // rows lie outside the cone of every value it hands on)
+        int64_t y = y0 + r;
+        if (WRAPY) {
+            y %= a.h;
+            if (y < 0) y += a.h;
+        } else if (y < a.ylo) {
+            y = a.ylo;
+        }
+        const uint64_t q = *reinterpret_cast<const uint64_t *>(row0 + y * a.pitch + voff);
+        ve[r] = (uint32_t)q;
+        vo[r] = (uint32_t)(q >> 32);
+    }
+    auto hsum = [&](uint32_t e, uint32_t o, uint32_t &e0, uint32_t &e1, uint32_t &o0, uint32_t &o1) {
+        BitEnc::pair_sums(e, o, bperm(laddr, o), bperm(raddr, e), e0, e1, o0, o1);
+    };
+    const bool last_wave = wi == NW - 1;
+    for (int g = 1; g <= m; ++g) {
+        const int par = g & 1;
+        // publish the old (generation g-1) last two rows: for the wave below,
+        // and from the last wave for the next tile (the ring, this tile's parity)
+        xs.x[par][wi][0][lane] = ve[R - 2];
+        xs.x[par][wi][1][lane] = vo[R - 2];
+        xs.x[par][wi][2][lane] = ve[R - 1];
+        xs.x[par][wi][3][lane] = vo[R - 1];
+        {
+            uint32_t(*dst)[64] = last_wave ? xs.ring[tpar][g - 1] : xs.sink;
+            dst[0][lane] = ve[R - 2];
+            dst[1][lane] = vo[R - 2];
+            dst[2][lane] = ve[R - 1];
+            dst[3][lane] = vo[R - 1];
+        }
+        // rows R-1 .. 2, bottom up: new_i = rule(h_{i-2}, h_{i-1}, h_i, old_{i-1})
+        uint32_t ae0, ae1, ao0, ao1;  // h_{i-2}
+        uint32_t be0, be1, bo0, bo1;  // h_{i-1}
+        uint32_t ce0, ce1, co0, co1;  // h_i
+        hsum(ve[R - 1], vo[R - 1], ce0, ce1, co0, co1);
+        hsum(ve[R - 2], vo[R - 2], be0, be1, bo0, bo1);
+        // the neighbour dwords of the next row are fetched one step ahead
+        uint32_t nl = bperm(laddr, vo[R - 3]), nr = bperm(raddr, ve[R - 3]);
+#pragma unroll
+        for (int i = R - 1; i >= 2; --i) {
+            const uint32_t cl = nl, cr = nr;
+            if (i >= 3) {
+                nl = bperm(laddr, vo[i - 3]);
+                nr = bperm(raddr, ve[i - 3]);
+            }
+            BitEnc::pair_sums(ve[i - 2], vo[i - 2], cl, cr, ae0, ae1, ao0, ao1);
+            ve[i] = BitEnc::rule1(ae0, ae1, be0, be1, ce0, ce1, ve[i - 1]);
+            vo[i] = BitEnc::rule1(ao0, ao1, bo0, bo1, co0, co1, vo[i - 1]);
+            ce0 = be0;
+            ce1 = be1;
+            co0 = bo0;
+            co1 = bo1;
+            be0 = ae0;
+            be1 = ae1;
+            bo0 = ao0;
+            bo1 = ao1;
+        }
+        // now b = h_0, c = h_1
+        __syncthreads();
+        // the two rows above: the wave above, or (wave 0) the tile above
+        // through the ring, or (a prologue's wave 0) zeros
+        // (a uniform pointer select and mask: no branch in the loop body)
+        const uint32_t(*src)[64] = wi > 0 ? xs.x[par][wi > 0 ? wi - 1 : 0] : xs.ring[tpar ^ 1][g - 1];
+        const uint32_t keep = (first && wi == 0) ? 0u : ~0u;
+        const uint32_t pe2 = src[0][lane] & keep, po2 = src[1][lane] & keep;
+        const uint32_t pe1 = src[2][lane] & keep, po1 = src[3][lane] & keep;
+        uint32_t me0, me1, mo0, mo1;  // h_{-1}
+        hsum(pe1, po1, me0, me1, mo0, mo1);
+        // row 1: rule(h_{-1}, h_0, h_1, old_0)
+        ve[1] = BitEnc::rule1(me0, me1, be0, be1, ce0, ce1, ve[0]);
+        vo[1] = BitEnc::rule1(mo0, mo1, bo0, bo1, co0, co1, vo[0]);
+        hsum(pe2, po2, ae0, ae1, ao0, ao1);  // h_{-2}
+        // row 0: rule(h_{-2}, h_{-1}, h_0, old_{-1})
+        ve[0] = BitEnc::rule1(ae0, ae1, me0, me1, be0, be1, pe1);
+        vo[0] = BitEnc::rule1(ao0, ao1, mo0, mo1, bo0, bo1, po1);
+    }
+    __syncthreads();  // the exchange slots and the ring are reused by the next tile
+    if (prologue) return;
+    // register row i of wave wi now holds domain row O + wi*R + i
+    int lane2 = (int)(threadIdx.x & 63);
+    asm volatile("" : "+v"(lane2));
+    const int64_t j2 = tx * 62 + lane2 - 1;
+    const bool st = (lane2 >= 1 && lane2 <= 62 && j2 < a.W) || (!WRAPX && a.xext && (j2 == -1 || j2 == a.W));
+    int64_t jl2;  // the load's column again: only the window lives across the loop
+    if (WRAPX) {
+        jl2 = j2 % a.W;
+        if (jl2 < 0) jl2 += a.W;
+    } else {
+        jl2 = j2 > a.W ? a.W : j2;
+    }
+    const int64_t yb = O + (int64_t)wi * R;
+    uint8_t *q = a.out + (a.ya + yb) * a.pitch + (uint32_t)(a.xoff + 8 * jl2);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (st && yb + r < a.h) *reinterpret_cast<uint64_t *>(q) = (uint64_t)ve[r] | ((uint64_t)vo[r] << 32);
+        q += a.pitch;
+    }
+}
+
+// One workgroup per segment: a prologue, then its tiles top to bottom.
+template <int R, bool WRAPX, bool WRAPY, int NW>
+__global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tskew_bit_kernel(KArgs a) {
+    __shared__ XchS<NW> xs;
+    const int64_t b = blockIdx.x;
+    const int64_t sc = b / a.ntx, tx = b % a.ntx;
+    const int64_t k0 = sc * a.seg, k1 = k0 + a.seg < a.nty ? k0 + a.seg : a.nty;
+    if (k0 >= k1) return;  // whole workgroup
+    const int64_t T = (int64_t)NW * R;
+    tile_body_skew<3, WRAPX, WRAPY, NW>(a, tx, k0 * T, xs, 0, true, true);
+    int tp = 1;
+    for (int64_t k = k0; k < k1; ++k, tp ^= 1) tile_body_skew<R, WRAPX, WRAPY, NW>(a, tx, k * T, xs, tp, false, false);
+}
+
 template <int R, int GK, bool WRAPX, bool WRAPY, int NW>
 __global__ __launch_bounds__(64 * NW, LIFE_BYTE_WPE) void tstep_byte_kernel(TArgs a) {
     __shared__ Xch<NW> xch;
@@ -1905,6 +2083,57 @@ hipError_t launch_tstep(const life_layout &Lin, const uint8_t *in, uint8_t *out,
                                             : byte_k<32>(wrap);
     if (!fn) return hipErrorInvalidValue;
     return launch_fn(fn, (unsigned)items, 64u * (unsigned)tile_waves(bit), &a, s, ev0, ev1);
+}
+
+// Skewed bit tiles (tskew_bit_kernel): the 24 x 8 shape only.
+namespace {
+const void *skew_fn(Wrap wrap) {
+    if (wrap.x && wrap.y) return (const void *)tskew_bit_kernel<24, true, true, 8>;
+    if (wrap.x) return (const void *)tskew_bit_kernel<24, true, false, 8>;
+    if (wrap.y) return (const void *)tskew_bit_kernel<24, false, true, 8>;
+    return (const void *)tskew_bit_kernel<24, false, false, 8>;
+}
+}  // namespace
+
+bool skew_ok(const life_layout &L, int m) {
+    return is_bit(L) && L.generations_per_exchange > 1 && m >= 1 && m <= 12 && temporal_rows(true) == 24 &&
+           tile_waves(true) == 8;
+}
+
+hipError_t launch_tskew(const life_layout &Lin, const uint8_t *in, uint8_t *out, int m, Wrap wrap, hipStream_t s,
+                        double *valu_lane_ops, hipEvent_t ev0, hipEvent_t ev1, Extend ext) {
+    const int K = Lin.generations_per_exchange;
+    if (!skew_ok(Lin, m) || m > K || Lin.yapron != K || ext.y < 0 || ext.y + m > K ||
+        (ext.y > 0 && wrap.y) || (ext.x && wrap.x))
+        return hipErrorInvalidValue;
+    const life_layout L = extended_layout(Lin, ext);
+    constexpr int64_t T = 24 * 8;  // rows per tile
+    KArgs a;
+    a.in = in;
+    a.out = out;
+    a.pitch = L.pitch;
+    a.xoff = L.xoff;
+    a.W = (L.w + 63) / 64;
+    a.h = L.h;
+    a.ya = L.yapron;
+    a.ylo = -L.yapron;
+    a.ntx = (a.W + 61) / 62;
+    a.nty = (L.h + T - 1) / T;
+    a.m = m;
+    a.xext = ext.x ? 1 : 0;
+    // one round of resident workgroups: each takes a segment of seg
+    // consecutive tiles of one column (one prologue per segment)
+    const void *fn = skew_fn(wrap);
+    static int cached[4] = {0, 0, 0, 0};
+    int &slots = cached[(wrap.x ? 2 : 0) + (wrap.y ? 1 : 0)];
+    if (slots == 0) slots = slots_of(fn, 64 * 8);
+    const int64_t tiles = a.ntx * a.nty;
+    a.seg = slots > 0 ? std::max<int64_t>(1, (tiles + slots - 1) / slots) : 1;
+    a.nsc = (a.nty + a.seg - 1) / a.seg;
+    const int64_t grid = a.ntx * a.nsc;
+    if (valu_lane_ops)  // per lane and generation: 24 rows x 22 + 12 (the two rows above), prologue 3 x 22 + 12
+        *valu_lane_ops = 64.0 * 8.0 * (double)m * ((double)tiles * (24.0 * 22.0 + 12.0) + (double)grid * (3.0 * 22.0 + 12.0));
+    return launch_fn(fn, (unsigned)grid, 64u * 8u, &a, s, ev0, ev1);
 }
 
 namespace {

@@ -444,3 +444,32 @@ def test_deep_halo_exchange_count(gpu, oracle, rccl):
             life.step(20)
             assert life.phase_stats()["blocks"] == blocks
             np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, 25, threads=4))
+
+
+# ---------------------------------------------------------------- skewed tiles (bit)
+@pytest.mark.parametrize("nx,ny,shards,dims", [
+    (4096, 1000, 1, (1, 1)), (64 * 63, 517, 1, (1, 1)), (2047, 200, 1, (1, 1)), (640, 24, 1, (1, 1)),
+    (8192, 4000, 1, (1, 1)), (1000, 70, 4, (2, 2)), (4100, 150, 2, (2, 1)), (512, 300, 4, (2, 2)),
+    (256, 400, 2, (1, 2))])
+@pytest.mark.parametrize("m", [12, 10, 7, 1])
+def test_skewed_tiles(gpu, oracle, nx, ny, shards, dims, m):
+    """LIFE_OPT_SKEW: whole-shard bit passes as time-skewed parallelogram
+    tiles (no ghost rows; a segment of tiles per workgroup fed through an LDS
+    ring, a 24-row prologue per segment) -- wrapped single shards with one or
+    many tile rows and segments, widths with a partial last pair, and the
+    deep-halo passes of partitioned shards (apron rows and pairs) -- against
+    the oracle, m = 1..12 generations per launch."""
+    if gpu.layout_query(nx, ny, dims, 0, "bit").generations_per_exchange == 1:
+        pytest.skip("one-generation layout")
+    g0 = oracle.fill_random(nx, ny, seed=nx + ny + m, density=0.45)
+    with gpu.Life(nx, ny, shards=shards, kernel="bit", dims=dims, transport=gpu.XPORT_LOCAL, small_grid=False,
+                  flow=0) as life:
+        life.configure(gpu.OPT_SKEW, 1)
+        life.configure(gpu.OPT_BLOCK_GENS, m)
+        life.upload(g0)
+        done = 0
+        for n in (m, 3 * m + 1, 40):
+            life.step(n)
+            done += n
+            np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, done, threads=4),
+                                          err_msg=f"after {done} generations")
