@@ -830,21 +830,25 @@ __device__ __forceinline__ void tile_body_skew(const KArgs &a, int64_t tx, int64
     const int64_t y0 = O + m + (int64_t)wi * R - (prologue ? (int64_t)NW * R : 0);
     const uint8_t *row0 = a.in + a.ya * a.pitch;
     uint32_t ve[R], vo[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        // one wave-uniform row per register row: wrapped, or clamped to the
-        // readable rows (only a prologue's top reaches above them, and those
-        // rows lie outside the cone of every value it hands on)
-        int64_t y = y0 + r;
+    {
+        // one wave-uniform row per register row, walked (no division per
+        // row): wrapped, or clamped to the readable rows (only a prologue's
+        // top reaches above them, and those rows lie outside the cone of
+        // every value it hands on)
+        int64_t y = y0;
         if (WRAPY) {
             y %= a.h;
             if (y < 0) y += a.h;
-        } else if (y < a.ylo) {
-            y = a.ylo;
         }
-        const uint64_t q = *reinterpret_cast<const uint64_t *>(row0 + y * a.pitch + voff);
-        ve[r] = (uint32_t)q;
-        vo[r] = (uint32_t)(q >> 32);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int64_t yy = (!WRAPY && y < a.ylo) ? a.ylo : y;
+            const uint64_t q = *reinterpret_cast<const uint64_t *>(row0 + yy * a.pitch + voff);
+            ve[r] = (uint32_t)q;
+            vo[r] = (uint32_t)(q >> 32);
+            ++y;
+            if (WRAPY && y == a.h) y = 0;
+        }
     }
     auto hsum = [&](uint32_t e, uint32_t o, uint32_t &e0, uint32_t &e1, uint32_t &o0, uint32_t &o1) {
         BitEnc::pair_sums(e, o, bperm(laddr, o), bperm(raddr, e), e0, e1, o0, o1);
