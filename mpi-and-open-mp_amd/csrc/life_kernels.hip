@@ -869,6 +869,10 @@ __device__ __forceinline__ void tile_body_skew(const KArgs &a, int64_t tx, int64
             dst[2][lane] = ve[R - 1];
             dst[3][lane] = vo[R - 1];
         }
+        // one barrier per generation, right after publishing (as the
+        // per-launch tiles): the reads of the rows above come at the sweep's
+        // end, their latency hidden behind it
+        __syncthreads();
         // rows R-1 .. 2, bottom up: new_i = rule(h_{i-2}, h_{i-1}, h_i, old_{i-1})
         uint32_t ae0, ae1, ao0, ao1;  // h_{i-2}
         uint32_t be0, be1, bo0, bo1;  // h_{i-1}
@@ -897,7 +901,6 @@ __device__ __forceinline__ void tile_body_skew(const KArgs &a, int64_t tx, int64
             bo1 = ao1;
         }
         // now b = h_0, c = h_1
-        __syncthreads();
         // the two rows above: the wave above, or (wave 0) the tile above
         // through the ring, or (a prologue's wave 0) zeros
         // (a uniform pointer select and mask: no branch in the loop body)
