@@ -792,7 +792,8 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tstep_bit_kernel(TArg
 // LDS: the inter-wave exchange holds the raw (E, O) of each wave's last two
 // rows per generation parity (16 KB at 8 waves), the ring the same four
 // dwords per generation for two tiles (tile parity: 24 KB): 40 KB, 3
-// workgroups per CU.
+// workgroups per CU.  (41 KB -- a 1 KB sink for the other waves' ring writes
+// -- measured as fast; kept at exactly the per-launch tiles' 40 KB.)
 struct KArgs {
     const uint8_t *in;
     uint8_t *out;
@@ -805,7 +806,6 @@ template <int NW>
 struct XchS {
     uint32_t x[2][NW][4][64];     // [gen parity][wave][E(R-2), O(R-2), E(R-1), O(R-1)][lane]
     uint32_t ring[2][12][4][64];  // [tile parity][generation - 1][same][lane]
-    uint32_t sink[4][64];         // the other waves' copy of the ring write (no branch)
 };
 
 template <int R, bool WRAPX, bool WRAPY, int NW>
@@ -863,7 +863,9 @@ __device__ __forceinline__ void tile_body_skew(const KArgs &a, int64_t tx, int64
         xs.x[par][wi][2][lane] = ve[R - 1];
         xs.x[par][wi][3][lane] = vo[R - 1];
         {
-            uint32_t(*dst)[64] = last_wave ? xs.ring[tpar][g - 1] : xs.sink;
+            // (the other waves write their exchange slot a second time: no
+            // branch, no extra LDS)
+            uint32_t(*dst)[64] = last_wave ? xs.ring[tpar][g - 1] : xs.x[par][wi];
             dst[0][lane] = ve[R - 2];
             dst[1][lane] = vo[R - 2];
             dst[2][lane] = ve[R - 1];
