@@ -801,6 +801,7 @@ struct KArgs {
     int64_t ylo;                    // lowest readable domain row (non-wrapped y: -ya)
     int64_t ntx, nty, seg, nsc;     // tile columns, tiles per column, tiles per segment, segments per column
     int32_t m, xext;
+    int32_t stagger;  // measurement knob (LIFE_SKEW_STAGGER): workgroup b first sleeps (b % 3) x stagger x 64 cycles
 };
 template <int NW>
 struct XchS {
@@ -952,6 +953,7 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tskew_bit_kernel(KArg
     const int64_t k0 = sc * a.seg, k1 = k0 + a.seg < a.nty ? k0 + a.seg : a.nty;
     if (k0 >= k1) return;  // whole workgroup
     const int64_t T = (int64_t)NW * R;
+    for (int i = 0; i < (int)(b % 3) * a.stagger; ++i) __builtin_amdgcn_s_sleep(1);
     tile_body_skew<3, WRAPX, WRAPY, NW>(a, tx, k0 * T, xs, 0, true, true);
     int tp = 1;
     for (int64_t k = k0; k < k1; ++k, tp ^= 1) tile_body_skew<R, WRAPX, WRAPY, NW>(a, tx, k * T, xs, tp, false, false);
@@ -2138,6 +2140,16 @@ hipError_t launch_tskew(const life_layout &Lin, const uint8_t *in, uint8_t *out,
     if (slots == 0) slots = slots_of(fn, 64 * 8);
     const int64_t tiles = a.ntx * a.nty;
     a.seg = slots > 0 ? std::max<int64_t>(1, (tiles + slots - 1) / slots) : 1;
+    static const int env_seg = [] {  // measurement knobs
+        const char *e = getenv("LIFE_SKEW_SEG");
+        return e ? atoi(e) : 0;
+    }();
+    static const int env_stagger = [] {
+        const char *e = getenv("LIFE_SKEW_STAGGER");
+        return e ? atoi(e) : 0;
+    }();
+    if (env_seg > 0) a.seg = env_seg;
+    a.stagger = env_stagger;
     a.nsc = (a.nty + a.seg - 1) / a.seg;
     const int64_t grid = a.ntx * a.nsc;
     if (valu_lane_ops)  // per lane and generation: 24 rows x 22 + 12 (the two rows above), prologue 3 x 22 + 12
