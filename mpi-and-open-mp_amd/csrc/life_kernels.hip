@@ -657,7 +657,7 @@ __device__ __forceinline__ void tile_body_byte(const TArgs &a, const uint8_t *in
             // LIFE_BYTE_LOAD_CHUNK rows of loads in flight at most: a
             // scheduling fence after every chunk keeps the load phase's
             // registers (8 per row in flight) inside the occupancy budget
-            if (LIFE_BYTE_LOAD_CHUNK > 0 && r > 0 && r % LIFE_BYTE_LOAD_CHUNK == 0)
+            if (LIFE_BYTE_LOAD_CHUNK > 0 && r > 0 && r % (LIFE_BYTE_LOAD_CHUNK > 0 ? LIFE_BYTE_LOAD_CHUNK : 1) == 0)
                 __builtin_amdgcn_sched_barrier(0);
             const uint4 *q = reinterpret_cast<const uint4 *>(p + voff);
             v[r] = pack32(q[0], q[1]);
@@ -794,6 +794,12 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tstep_bit_kernel(TArg
 // dwords per generation for two tiles (tile parity: 24 KB): 40 KB, 3
 // workgroups per CU.  (41 KB -- a 1 KB sink for the other waves' ring writes
 // -- measured as fast; kept at exactly the per-launch tiles' 40 KB.)
+// LIFE_SKEW_FENCE (compile time, A/B): 0 lets the compiler sink each
+// generation's barrier to the end of the sweep, 1 pins it after the publish,
+// 2 also reads the rows above right after it.
+#ifndef LIFE_SKEW_FENCE
+#define LIFE_SKEW_FENCE 0
+#endif
 struct KArgs {
     const uint8_t *in;
     uint8_t *out;
@@ -876,6 +882,19 @@ __device__ __forceinline__ void tile_body_skew(const KArgs &a, int64_t tx, int64
         // per-launch tiles): the reads of the rows above come at the sweep's
         // end, their latency hidden behind it
         __syncthreads();
+        // the two rows above: the wave above, or (wave 0) the tile above
+        // through the ring, or (a prologue's wave 0) zeros
+        // (a uniform pointer select and mask: no branch in the loop body)
+        uint32_t pe2, po2, pe1, po1;
+        if (LIFE_SKEW_FENCE >= 2) {
+            const uint32_t(*src)[64] = wi > 0 ? xs.x[par][wi > 0 ? wi - 1 : 0] : xs.ring[tpar ^ 1][g - 1];
+            const uint32_t keep = (first && wi == 0) ? 0u : ~0u;
+            pe2 = src[0][lane] & keep;
+            po2 = src[1][lane] & keep;
+            pe1 = src[2][lane] & keep;
+            po1 = src[3][lane] & keep;
+        }
+        if (LIFE_SKEW_FENCE >= 1) __builtin_amdgcn_sched_barrier(0);
         // rows R-1 .. 2, bottom up: new_i = rule(h_{i-2}, h_{i-1}, h_i, old_{i-1})
         uint32_t ae0, ae1, ao0, ao1;  // h_{i-2}
         uint32_t be0, be1, bo0, bo1;  // h_{i-1}
@@ -904,13 +923,14 @@ __device__ __forceinline__ void tile_body_skew(const KArgs &a, int64_t tx, int64
             bo1 = ao1;
         }
         // now b = h_0, c = h_1
-        // the two rows above: the wave above, or (wave 0) the tile above
-        // through the ring, or (a prologue's wave 0) zeros
-        // (a uniform pointer select and mask: no branch in the loop body)
-        const uint32_t(*src)[64] = wi > 0 ? xs.x[par][wi > 0 ? wi - 1 : 0] : xs.ring[tpar ^ 1][g - 1];
-        const uint32_t keep = (first && wi == 0) ? 0u : ~0u;
-        const uint32_t pe2 = src[0][lane] & keep, po2 = src[1][lane] & keep;
-        const uint32_t pe1 = src[2][lane] & keep, po1 = src[3][lane] & keep;
+        if (LIFE_SKEW_FENCE < 2) {
+            const uint32_t(*src)[64] = wi > 0 ? xs.x[par][wi > 0 ? wi - 1 : 0] : xs.ring[tpar ^ 1][g - 1];
+            const uint32_t keep = (first && wi == 0) ? 0u : ~0u;
+            pe2 = src[0][lane] & keep;
+            po2 = src[1][lane] & keep;
+            pe1 = src[2][lane] & keep;
+            po1 = src[3][lane] & keep;
+        }
         uint32_t me0, me1, mo0, mo1;  // h_{-1}
         hsum(pe1, po1, me0, me1, mo0, mo1);
         // row 1: rule(h_{-1}, h_0, h_1, old_0)
