@@ -32,6 +32,27 @@
 
 namespace life {
 namespace {
+// LIFE_WG_TRACE (compile time, diagnostics builds only): thread 0 of every
+// workgroup of the bit tile kernels records [start, end, HW_ID | XCC_ID << 32]
+// (wall clock, 100 MHz) for the last launch; life_debug_wg_trace copies it out.
+#ifndef LIFE_WG_TRACE
+#define LIFE_WG_TRACE 0
+#endif
+#if LIFE_WG_TRACE
+__device__ uint64_t g_wg_trace[3 * 65536];
+__device__ __forceinline__ void wg_trace(int what) {
+    if (threadIdx.x != 0 || blockIdx.x >= 65536) return;
+    uint64_t *t = g_wg_trace + 3 * blockIdx.x;
+    t[what] = wall_clock64();
+    if (what == 0) {
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);
+        t[2] = (uint64_t)hw | ((uint64_t)xcc << 32);
+    }
+}
+#else
+__device__ __forceinline__ void wg_trace(int) {}
+#endif
 
 constexpr int kBlock = 256;  // 4 waves of 64
 
@@ -737,6 +758,7 @@ constexpr int bit_wpe(int NW, int R) { return NW == 16 ? (R <= 16 ? 8 : 4) : (R 
 template <int R, bool WRAPX, bool WRAPY, int NW>
 __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tstep_bit_kernel(TArgs a) {
     __shared__ XchB<NW> xch;
+    wg_trace(0);
     int64_t wg = blockIdx.x;
     if (wg < a.xcd_n) {
         // the dispatcher deals blocks round-robin over the 8 XCDs: XCD x runs
@@ -750,6 +772,7 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tstep_bit_kernel(TArg
         const int64_t i = wg - a.half_first;
         tile_body_bit<R / 2, WRAPX, WRAPY, 0, NW>(a, a.in, a.out, i % a.half_ntx, i / a.half_ntx, xch, 6, 1,
                                                   a.half_y, a.half_yend);
+        wg_trace(1);
         return;
     }
     const int64_t nwg = a.first[a.nreg];
@@ -768,6 +791,7 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tstep_bit_kernel(TArg
         const int nb = (int)(a.ty1[k] - ty < B ? a.ty1[k] - ty : B);
         tile_body_bit<R, WRAPX, WRAPY, 0, NW, true>(a, a.in, a.out, a.bcol, ty, xch, a.gsh, nb);
     }
+    wg_trace(1);
 }
 
 // ------------------------------------------------------------------ skewed bit tiles
@@ -796,7 +820,8 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tstep_bit_kernel(TArg
 // -- measured as fast; kept at exactly the per-launch tiles' 40 KB.)
 // LIFE_SKEW_FENCE (compile time, A/B): 0 lets the compiler sink each
 // generation's barrier to the end of the sweep, 1 pins it after the publish,
-// 2 also reads the rows above right after it.
+// 2 also reads the rows above right after it, 3 also fetches their
+// neighbour dwords there.
 #ifndef LIFE_SKEW_FENCE
 #define LIFE_SKEW_FENCE 0
 #endif
@@ -885,7 +910,7 @@ __device__ __forceinline__ void tile_body_skew(const KArgs &a, int64_t tx, int64
         // the two rows above: the wave above, or (wave 0) the tile above
         // through the ring, or (a prologue's wave 0) zeros
         // (a uniform pointer select and mask: no branch in the loop body)
-        uint32_t pe2, po2, pe1, po1;
+        uint32_t pe2, po2, pe1, po1, pl1 = 0, pr1 = 0, pl2 = 0, pr2 = 0;
         if (LIFE_SKEW_FENCE >= 2) {
             const uint32_t(*src)[64] = wi > 0 ? xs.x[par][wi > 0 ? wi - 1 : 0] : xs.ring[tpar ^ 1][g - 1];
             const uint32_t keep = (first && wi == 0) ? 0u : ~0u;
@@ -893,6 +918,12 @@ __device__ __forceinline__ void tile_body_skew(const KArgs &a, int64_t tx, int64
             po2 = src[1][lane] & keep;
             pe1 = src[2][lane] & keep;
             po1 = src[3][lane] & keep;
+            if (LIFE_SKEW_FENCE >= 3) {
+                pl1 = bperm(laddr, po1);
+                pr1 = bperm(raddr, pe1);
+                pl2 = bperm(laddr, po2);
+                pr2 = bperm(raddr, pe2);
+            }
         }
         if (LIFE_SKEW_FENCE >= 1) __builtin_amdgcn_sched_barrier(0);
         // rows R-1 .. 2, bottom up: new_i = rule(h_{i-2}, h_{i-1}, h_i, old_{i-1})
@@ -932,11 +963,17 @@ __device__ __forceinline__ void tile_body_skew(const KArgs &a, int64_t tx, int64
             po1 = src[3][lane] & keep;
         }
         uint32_t me0, me1, mo0, mo1;  // h_{-1}
-        hsum(pe1, po1, me0, me1, mo0, mo1);
+        if (LIFE_SKEW_FENCE >= 3)
+            BitEnc::pair_sums(pe1, po1, pl1, pr1, me0, me1, mo0, mo1);
+        else
+            hsum(pe1, po1, me0, me1, mo0, mo1);
         // row 1: rule(h_{-1}, h_0, h_1, old_0)
         ve[1] = BitEnc::rule1(me0, me1, be0, be1, ce0, ce1, ve[0]);
         vo[1] = BitEnc::rule1(mo0, mo1, bo0, bo1, co0, co1, vo[0]);
-        hsum(pe2, po2, ae0, ae1, ao0, ao1);  // h_{-2}
+        if (LIFE_SKEW_FENCE >= 3)  // h_{-2}
+            BitEnc::pair_sums(pe2, po2, pl2, pr2, ae0, ae1, ao0, ao1);
+        else
+            hsum(pe2, po2, ae0, ae1, ao0, ao1);
         // row 0: rule(h_{-2}, h_{-1}, h_0, old_{-1})
         ve[0] = BitEnc::rule1(ae0, ae1, me0, me1, be0, be1, pe1);
         vo[0] = BitEnc::rule1(ao0, ao1, mo0, mo1, bo0, bo1, po1);
@@ -968,6 +1005,7 @@ __device__ __forceinline__ void tile_body_skew(const KArgs &a, int64_t tx, int64
 template <int R, bool WRAPX, bool WRAPY, int NW>
 __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tskew_bit_kernel(KArgs a) {
     __shared__ XchS<NW> xs;
+    wg_trace(0);
     const int64_t b = blockIdx.x;
     const int64_t sc = b / a.ntx, tx = b % a.ntx;
     const int64_t k0 = sc * a.seg, k1 = k0 + a.seg < a.nty ? k0 + a.seg : a.nty;
@@ -977,6 +1015,7 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tskew_bit_kernel(KArg
     tile_body_skew<3, WRAPX, WRAPY, NW>(a, tx, k0 * T, xs, 0, true, true);
     int tp = 1;
     for (int64_t k = k0; k < k1; ++k, tp ^= 1) tile_body_skew<R, WRAPX, WRAPY, NW>(a, tx, k * T, xs, tp, false, false);
+    wg_trace(1);
 }
 
 template <int R, int GK, bool WRAPX, bool WRAPY, int NW>
@@ -2469,3 +2508,14 @@ hipError_t launch_census(const life_layout &L, int64_t nx, const uint8_t *buf, u
 }
 
 }  // namespace life
+
+#if LIFE_WG_TRACE
+// Diagnostics builds only: the per-workgroup trace of the last bit tile launch.
+extern "C" int life_debug_wg_trace(uint64_t *host, int64_t n) {
+    if (n > 3 * 65536) n = 3 * 65536;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(life::g_wg_trace), n * sizeof(uint64_t), 0, hipMemcpyDeviceToHost) ==
+                   hipSuccess
+               ? 0
+               : -1;
+}
+#endif
