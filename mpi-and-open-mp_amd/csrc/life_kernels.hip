@@ -33,21 +33,22 @@
 namespace life {
 namespace {
 // LIFE_WG_TRACE (compile time, diagnostics builds only): thread 0 of every
-// workgroup of the bit tile kernels records [start, end, HW_ID | XCC_ID << 32]
-// (wall clock, 100 MHz) for the last launch; life_debug_wg_trace copies it out.
+// workgroup of the bit tile kernels records [start, HW_ID | XCC_ID << 32, end
+// of each tile (up to 14)] (wall clock, 100 MHz) for the last launch;
+// life_debug_wg_trace copies it out.
 #ifndef LIFE_WG_TRACE
 #define LIFE_WG_TRACE 0
 #endif
 #if LIFE_WG_TRACE
-__device__ uint64_t g_wg_trace[3 * 65536];
-__device__ __forceinline__ void wg_trace(int what) {
-    if (threadIdx.x != 0 || blockIdx.x >= 65536) return;
-    uint64_t *t = g_wg_trace + 3 * blockIdx.x;
-    t[what] = wall_clock64();
+__device__ uint64_t g_wg_trace[16 * 65536];
+__device__ __forceinline__ void wg_trace(int what) {  // 0: start, k >= 1: end of tile k
+    if (threadIdx.x != 0 || blockIdx.x >= 65536 || what > 14) return;
+    uint64_t *t = g_wg_trace + 16 * blockIdx.x;
+    t[what == 0 ? 0 : what + 1] = wall_clock64();
     if (what == 0) {
         const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
         const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);
-        t[2] = (uint64_t)hw | ((uint64_t)xcc << 32);
+        t[1] = (uint64_t)hw | ((uint64_t)xcc << 32);
     }
 }
 #else
@@ -825,6 +826,9 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tstep_bit_kernel(TArg
 #ifndef LIFE_SKEW_FENCE
 #define LIFE_SKEW_FENCE 0
 #endif
+#ifndef LIFE_SKEW_PRIO
+#define LIFE_SKEW_PRIO 0
+#endif
 struct KArgs {
     const uint8_t *in;
     uint8_t *out;
@@ -1014,8 +1018,22 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tskew_bit_kernel(KArg
     for (int i = 0; i < (int)(b % 3) * a.stagger; ++i) __builtin_amdgcn_s_sleep(1);
     tile_body_skew<3, WRAPX, WRAPY, NW>(a, tx, k0 * T, xs, 0, true, true);
     int tp = 1;
-    for (int64_t k = k0; k < k1; ++k, tp ^= 1) tile_body_skew<R, WRAPX, WRAPY, NW>(a, tx, k * T, xs, tp, false, false);
-    wg_trace(1);
+    for (int64_t k = k0; k < k1; ++k, tp ^= 1) {
+        if (LIFE_SKEW_PRIO) {
+            // the workgroups sharing a CU advance together: issue priority
+            // falls as a segment progresses (the arbiter otherwise favours
+            // the oldest waves: the CU's first workgroup finishes first and
+            // the last runs its tail alone)
+            switch ((int)(4 * (k - k0) / a.seg)) {
+            case 0: __builtin_amdgcn_s_setprio(3); break;
+            case 1: __builtin_amdgcn_s_setprio(2); break;
+            case 2: __builtin_amdgcn_s_setprio(1); break;
+            default: __builtin_amdgcn_s_setprio(0); break;
+            }
+        }
+        tile_body_skew<R, WRAPX, WRAPY, NW>(a, tx, k * T, xs, tp, false, false);
+        wg_trace((int)(k - k0) + 1);
+    }
 }
 
 template <int R, int GK, bool WRAPX, bool WRAPY, int NW>
@@ -2512,7 +2530,7 @@ hipError_t launch_census(const life_layout &L, int64_t nx, const uint8_t *buf, u
 #if LIFE_WG_TRACE
 // Diagnostics builds only: the per-workgroup trace of the last bit tile launch.
 extern "C" int life_debug_wg_trace(uint64_t *host, int64_t n) {
-    if (n > 3 * 65536) n = 3 * 65536;
+    if (n > 16 * 65536) n = 16 * 65536;
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(life::g_wg_trace), n * sizeof(uint64_t), 0, hipMemcpyDeviceToHost) ==
                    hipSuccess
                ? 0

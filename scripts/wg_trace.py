@@ -21,18 +21,19 @@ with lm.Life(65536, 65536, shards=1, kernel="bit") as life:
     life.step(gens)
     life.live_count()
     L = lm._lib()
-    n = 3 * 65536
+    n = 16 * 65536
     buf = (ctypes.c_uint64 * n)()
     fn = L.life_debug_wg_trace
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int64]
     assert fn(buf, n) == 0
-t = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 3)
+t = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 16)
 t = t[t[:, 0] > 0]
 t0 = int(t[:, 0].min())
 start = (t[:, 0].astype(np.int64) - t0) / 100.0  # us
-end = (t[:, 1].astype(np.int64) - t0) / 100.0
-hw = t[:, 2] & 0xFFFFFFFF
-xcc = (t[:, 2] >> 32) & 0xF
+tiles = np.where(t[:, 2:] > 0, (t[:, 2:].astype(np.int64) - t0) / 100.0, np.nan)  # end of each tile
+end = np.nanmax(tiles, axis=1)
+hw = t[:, 1] & 0xFFFFFFFF
+xcc = (t[:, 1] >> 32) & 0xF
 cu = (hw >> 8) & 0xF
 sh = (hw >> 12) & 1
 se = (hw >> 13) & 0x7
@@ -62,5 +63,9 @@ share = np.array([int(((cuid == cuid[i]) & (start <= mid[i]) & (end > mid[i])).s
 for s_ in np.unique(share):
     m = share == s_
     print(f"  sharing {s_}: {m.sum()} workgroups, median dur {np.median(dur[m]):.1f} us")
+ntile = np.sum(~np.isnan(tiles), axis=1)
+if ntile.max() > 1:  # skewed segments: time per tile (the first includes the prologue)
+    per = np.diff(np.concatenate([start[:, None], tiles], 1), axis=1)
+    print("per tile median by position:", [round(float(np.nanmedian(per[:, k])), 1) for k in range(int(ntile.max()))])
 if len(sys.argv) > 2:
-    np.save(sys.argv[2], np.stack([start, end, cuid, xcc], 1))
+    np.save(sys.argv[2], np.concatenate([np.stack([start, end, cuid, xcc], 1), tiles], 1))
