@@ -829,6 +829,9 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tstep_bit_kernel(TArg
 #ifndef LIFE_SKEW_PRIO
 #define LIFE_SKEW_PRIO 0
 #endif
+#ifndef LIFE_SKEW_XCD
+#define LIFE_SKEW_XCD 0
+#endif
 struct KArgs {
     const uint8_t *in;
     uint8_t *out;
@@ -1010,7 +1013,15 @@ template <int R, bool WRAPX, bool WRAPY, int NW>
 __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tskew_bit_kernel(KArgs a) {
     __shared__ XchS<NW> xs;
     wg_trace(0);
-    const int64_t b = blockIdx.x;
+    int64_t b = blockIdx.x;
+    if (LIFE_SKEW_XCD) {
+        // the dispatcher deals blocks round-robin over the 8 XCDs: XCD x runs
+        // blocks 8k + x, here segments first_x + k, so a segment row's tile
+        // columns share one L2 (each 512-B row piece straddles the 128-B
+        // lines it shares with the next column: fetched once, not twice)
+        const int64_t n = a.ntx * a.nsc, x = b & 7, k = b >> 3, per = n >> 3, rem = n & 7;
+        b = (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + k;
+    }
     const int64_t sc = b / a.ntx, tx = b % a.ntx;
     const int64_t k0 = sc * a.seg, k1 = k0 + a.seg < a.nty ? k0 + a.seg : a.nty;
     if (k0 >= k1) return;  // whole workgroup
