@@ -817,21 +817,21 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tstep_bit_kernel(TArg
 // LDS: the inter-wave exchange holds the raw (E, O) of each wave's last two
 // rows per generation parity (16 KB at 8 waves), the ring the same four
 // dwords per generation for two tiles (tile parity: 24 KB): 40 KB, 3
-// workgroups per CU.  (41 KB -- a 1 KB sink for the other waves' ring writes
-// -- measured as fast; kept at exactly the per-launch tiles' 40 KB.)
-// LIFE_SKEW_FENCE (compile time, A/B): 0 lets the compiler sink each
-// generation's barrier to the end of the sweep, 1 pins it after the publish,
-// 2 also reads the rows above right after it, 3 also fetches their
-// neighbour dwords there.
-#ifndef LIFE_SKEW_FENCE
-#define LIFE_SKEW_FENCE 0
-#endif
-#ifndef LIFE_SKEW_PRIO
-#define LIFE_SKEW_PRIO 0
-#endif
-#ifndef LIFE_SKEW_XCD
-#define LIFE_SKEW_XCD 0
-#endif
+// workgroups per CU, as the per-launch tiles.
+//
+// Measured (65536^2, driver-shaped call; DESIGN.md 5.1, profiles/r04/k-t):
+// parity green, but 0.450 ms per launch against 0.416 for tile_body_bit.
+// With all three workgroups of a CU resident a skewed tile costs 5 % less
+// per owned row than a per-launch tile (16.5 vs 15.6 us per tile per CU,
+// 192 vs 172 owned rows); what it loses is the tail: one workgroup per
+// segment means one round of 731 workgroups, the CU's oldest workgroup
+// issues first and finishes first, and the last third of the launch runs
+// with one or two workgroups per CU (scripts/wg_trace.py).  Opt-in
+// (LIFE_OPT_SKEW / LIFE_SKEW=1).  The three measured fixes kept below: the
+// barrier pinned after the publish with the rows above read right after it
+// (the compiler otherwise sank it to the sweep's end: 0.50 -> 0.48 ms),
+// segments dealt XCD-aware (HBM fetch 1.23x -> 1.02x of the per-launch
+// tiles'), issue priority falling along a segment (0.48 -> 0.45 ms).
 struct KArgs {
     const uint8_t *in;
     uint8_t *out;
@@ -839,7 +839,6 @@ struct KArgs {
     int64_t ylo;                    // lowest readable domain row (non-wrapped y: -ya)
     int64_t ntx, nty, seg, nsc;     // tile columns, tiles per column, tiles per segment, segments per column
     int32_t m, xext;
-    int32_t stagger;  // measurement knob (LIFE_SKEW_STAGGER): workgroup b first sleeps (b % 3) x stagger x 64 cycles
 };
 template <int NW>
 struct XchS {
@@ -917,22 +916,16 @@ __device__ __forceinline__ void tile_body_skew(const KArgs &a, int64_t tx, int64
         // the two rows above: the wave above, or (wave 0) the tile above
         // through the ring, or (a prologue's wave 0) zeros
         // (a uniform pointer select and mask: no branch in the loop body)
-        uint32_t pe2, po2, pe1, po1, pl1 = 0, pr1 = 0, pl2 = 0, pr2 = 0;
-        if (LIFE_SKEW_FENCE >= 2) {
-            const uint32_t(*src)[64] = wi > 0 ? xs.x[par][wi > 0 ? wi - 1 : 0] : xs.ring[tpar ^ 1][g - 1];
-            const uint32_t keep = (first && wi == 0) ? 0u : ~0u;
-            pe2 = src[0][lane] & keep;
-            po2 = src[1][lane] & keep;
-            pe1 = src[2][lane] & keep;
-            po1 = src[3][lane] & keep;
-            if (LIFE_SKEW_FENCE >= 3) {
-                pl1 = bperm(laddr, po1);
-                pr1 = bperm(raddr, pe1);
-                pl2 = bperm(laddr, po2);
-                pr2 = bperm(raddr, pe2);
-            }
-        }
-        if (LIFE_SKEW_FENCE >= 1) __builtin_amdgcn_sched_barrier(0);
+        // (read here, with their neighbour dwords, and used at the sweep's
+        // end; the scheduling fence keeps the compiler from sinking the
+        // barrier to the sweep's end)
+        const uint32_t(*src)[64] = wi > 0 ? xs.x[par][wi > 0 ? wi - 1 : 0] : xs.ring[tpar ^ 1][g - 1];
+        const uint32_t keep = (first && wi == 0) ? 0u : ~0u;
+        const uint32_t pe2 = src[0][lane] & keep, po2 = src[1][lane] & keep;
+        const uint32_t pe1 = src[2][lane] & keep, po1 = src[3][lane] & keep;
+        const uint32_t pl1 = bperm(laddr, po1), pr1 = bperm(raddr, pe1);
+        const uint32_t pl2 = bperm(laddr, po2), pr2 = bperm(raddr, pe2);
+        __builtin_amdgcn_sched_barrier(0);
         // rows R-1 .. 2, bottom up: new_i = rule(h_{i-2}, h_{i-1}, h_i, old_{i-1})
         uint32_t ae0, ae1, ao0, ao1;  // h_{i-2}
         uint32_t be0, be1, bo0, bo1;  // h_{i-1}
@@ -961,26 +954,12 @@ __device__ __forceinline__ void tile_body_skew(const KArgs &a, int64_t tx, int64
             bo1 = ao1;
         }
         // now b = h_0, c = h_1
-        if (LIFE_SKEW_FENCE < 2) {
-            const uint32_t(*src)[64] = wi > 0 ? xs.x[par][wi > 0 ? wi - 1 : 0] : xs.ring[tpar ^ 1][g - 1];
-            const uint32_t keep = (first && wi == 0) ? 0u : ~0u;
-            pe2 = src[0][lane] & keep;
-            po2 = src[1][lane] & keep;
-            pe1 = src[2][lane] & keep;
-            po1 = src[3][lane] & keep;
-        }
         uint32_t me0, me1, mo0, mo1;  // h_{-1}
-        if (LIFE_SKEW_FENCE >= 3)
-            BitEnc::pair_sums(pe1, po1, pl1, pr1, me0, me1, mo0, mo1);
-        else
-            hsum(pe1, po1, me0, me1, mo0, mo1);
+        BitEnc::pair_sums(pe1, po1, pl1, pr1, me0, me1, mo0, mo1);
         // row 1: rule(h_{-1}, h_0, h_1, old_0)
         ve[1] = BitEnc::rule1(me0, me1, be0, be1, ce0, ce1, ve[0]);
         vo[1] = BitEnc::rule1(mo0, mo1, bo0, bo1, co0, co1, vo[0]);
-        if (LIFE_SKEW_FENCE >= 3)  // h_{-2}
-            BitEnc::pair_sums(pe2, po2, pl2, pr2, ae0, ae1, ao0, ao1);
-        else
-            hsum(pe2, po2, ae0, ae1, ao0, ao1);
+        BitEnc::pair_sums(pe2, po2, pl2, pr2, ae0, ae1, ao0, ao1);  // h_{-2}
         // row 0: rule(h_{-2}, h_{-1}, h_0, old_{-1})
         ve[0] = BitEnc::rule1(ae0, ae1, me0, me1, be0, be1, pe1);
         vo[0] = BitEnc::rule1(ao0, ao1, mo0, mo1, bo0, bo1, po1);
@@ -1014,7 +993,7 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tskew_bit_kernel(KArg
     __shared__ XchS<NW> xs;
     wg_trace(0);
     int64_t b = blockIdx.x;
-    if (LIFE_SKEW_XCD) {
+    {
         // the dispatcher deals blocks round-robin over the 8 XCDs: XCD x runs
         // blocks 8k + x, here segments first_x + k, so a segment row's tile
         // columns share one L2 (each 512-B row piece straddles the 128-B
@@ -1026,21 +1005,18 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tskew_bit_kernel(KArg
     const int64_t k0 = sc * a.seg, k1 = k0 + a.seg < a.nty ? k0 + a.seg : a.nty;
     if (k0 >= k1) return;  // whole workgroup
     const int64_t T = (int64_t)NW * R;
-    for (int i = 0; i < (int)(b % 3) * a.stagger; ++i) __builtin_amdgcn_s_sleep(1);
     tile_body_skew<3, WRAPX, WRAPY, NW>(a, tx, k0 * T, xs, 0, true, true);
     int tp = 1;
     for (int64_t k = k0; k < k1; ++k, tp ^= 1) {
-        if (LIFE_SKEW_PRIO) {
-            // the workgroups sharing a CU advance together: issue priority
-            // falls as a segment progresses (the arbiter otherwise favours
-            // the oldest waves: the CU's first workgroup finishes first and
-            // the last runs its tail alone)
-            switch ((int)(4 * (k - k0) / a.seg)) {
-            case 0: __builtin_amdgcn_s_setprio(3); break;
-            case 1: __builtin_amdgcn_s_setprio(2); break;
-            case 2: __builtin_amdgcn_s_setprio(1); break;
-            default: __builtin_amdgcn_s_setprio(0); break;
-            }
+        // the workgroups sharing a CU advance together: issue priority falls
+        // as a segment progresses (the arbiter otherwise favours the oldest
+        // waves: the CU's first workgroup finishes first and the last runs
+        // its tail alone)
+        switch ((int)(4 * (k - k0) / a.seg)) {
+        case 0: __builtin_amdgcn_s_setprio(3); break;
+        case 1: __builtin_amdgcn_s_setprio(2); break;
+        case 2: __builtin_amdgcn_s_setprio(1); break;
+        default: __builtin_amdgcn_s_setprio(0); break;
         }
         tile_body_skew<R, WRAPX, WRAPY, NW>(a, tx, k * T, xs, tp, false, false);
         wg_trace((int)(k - k0) + 1);
@@ -2228,16 +2204,7 @@ hipError_t launch_tskew(const life_layout &Lin, const uint8_t *in, uint8_t *out,
     if (slots == 0) slots = slots_of(fn, 64 * 8);
     const int64_t tiles = a.ntx * a.nty;
     a.seg = slots > 0 ? std::max<int64_t>(1, (tiles + slots - 1) / slots) : 1;
-    static const int env_seg = [] {  // measurement knobs
-        const char *e = getenv("LIFE_SKEW_SEG");
-        return e ? atoi(e) : 0;
-    }();
-    static const int env_stagger = [] {
-        const char *e = getenv("LIFE_SKEW_STAGGER");
-        return e ? atoi(e) : 0;
-    }();
-    if (env_seg > 0) a.seg = env_seg;
-    a.stagger = env_stagger;
+
     a.nsc = (a.nty + a.seg - 1) / a.seg;
     const int64_t grid = a.ntx * a.nsc;
     if (valu_lane_ops)  // per lane and generation: 24 rows x 22 + 12 (the two rows above), prologue 3 x 22 + 12
