@@ -2132,11 +2132,9 @@ hipError_t launch_tstep(const life_layout &Lin, const uint8_t *in, uint8_t *out,
         const int slots = tstep_bit_slots();
         const int64_t rem = slots > 0 ? items % slots : 0;
         const int64_t ty0 = a.ty0[0], ty1 = a.ty1[0], yend = std::min(ty1 * g.rows, L.h);
-        static const int tail_mode = [] {  // measurement knob: 1 = split whatever the last round's fill
-            const char *e = getenv("LIFE_TAIL_MODE");
-            return e ? atoi(e) : 0;
-        }();
-        if (slots > 0 && items > slots && rem != 0 && (rem <= slots / 2 || tail_mode == 1)) {
+        // (Splitting whatever the last round's fill measured 1-3 % slower,
+        // profiles/r04/tail_u.)
+        if (slots > 0 && items > slots && rem != 0 && rem <= slots / 2) {
             int64_t q = 1;
             while (q < ty1 - ty0 && ((q * g.rows + T2 - 1) / T2) * g.ntx < slots) ++q;
             if (q < ty1 - ty0) {
