@@ -122,6 +122,13 @@ def test_timing_stats(gpu, kernel, nx, gens, flow):
             for m in sizes:
                 ghost = m if kernel == "bit" else K  # byte tiles: compile-time ghost depth K
                 nty = -(-4096 // (NW * R - 2 * ghost))
+                if kernel == "bit" and not flow and os.environ.get("LIFE_SKEW") == "1" and m <= 12:
+                    # skewed tiles (launch_tskew): 192-row tiles partition the rows, 2 tile columns, one
+                    # segment (prologue) per tile at this size; 24 rows x 22 + 12 per wave and generation,
+                    # the prologue 3 x 22 + 12
+                    tiles = 2 * -(-4096 // (NW * R))
+                    want += 64 * NW * m * tiles * ((R * 22 + 12) + (3 * 22 + 12))
+                    continue
                 if kernel == "bit":
                     # 64 pairs per row: two tile columns, the second owning 2 pairs; per-launch tiles run it as
                     # bands of 4 lanes, 16 tile rows per workgroup (life_kernels.hip tile_geom / region_items;
