@@ -839,7 +839,6 @@ struct KArgs {
     int64_t ylo;                    // lowest readable domain row (non-wrapped y: -ya)
     int64_t ntx, nty, seg, nsc;     // tile columns, tiles per column, tiles per segment, segments per column
     int32_t m, xext;
-    uint32_t epoch;  // launch tag of the progress table entries (LIFE_SKEW_BALANCE)
 };
 template <int NW>
 struct XchS {
@@ -847,51 +846,9 @@ struct XchS {
     uint32_t ring[2][12][4][64];  // [tile parity][generation - 1][same][lane]
 };
 
-// LIFE_SKEW_BALANCE (compile time, A/B): progress-balanced issue priority.
-// Every wave publishes its workgroup's progress (generations done in the
-// segment) each generation into a per-CU table slot keyed by its own
-// hardware wave slot, reads its CU's 64 slots, and takes priority 3 when no
-// workgroup on the CU is behind it, 1 when one is, 0 when two are: the
-// workgroups sharing a CU advance together and finish together.  A hint
-// only: stale or foreign entries change the schedule, never the result.
-#ifndef LIFE_SKEW_BALANCE
-#define LIFE_SKEW_BALANCE 0
-#endif
-#if LIFE_SKEW_BALANCE
-__device__ uint64_t g_skew_prog[2048 * 64];  // [CU][SIMD x 16 + wave slot]: epoch << 32 | progress
-struct SkewBal {
-    uint64_t *cu;  // this CU's 64 slots
-    uint64_t *me;  // this wave's slot
-    uint64_t tag;  // epoch << 32
-};
-__device__ __forceinline__ SkewBal skew_bal(uint32_t epoch) {
-    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_ID
-    const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20) & 7;  // XCC_ID
-    const uint32_t cu = ((xcc * 8 + ((hw >> 13) & 7)) * 2 + ((hw >> 12) & 1)) * 16 + ((hw >> 8) & 15);
-    SkewBal b;
-    b.cu = g_skew_prog + (size_t)cu * 64;
-    b.me = b.cu + (((hw >> 4) & 3) * 16 + (hw & 15));
-    b.tag = (uint64_t)epoch << 32;
-    return b;
-}
-__device__ __forceinline__ void skew_publish(const SkewBal &b, uint32_t progress) {
-    *b.me = b.tag | progress;  // every lane, one address, one value
-}
-// priority from the table entries read one generation earlier
-__device__ __forceinline__ void skew_prio(const SkewBal &b, uint64_t seen, uint32_t progress) {
-    const bool behind = (seen >> 32) == (b.tag >> 32) && (uint32_t)seen < progress;
-    const int n = __popcll(__ballot(behind)) >> 3;  // 8 waves (slots) per workgroup behind
-    switch (n) {
-    case 0: __builtin_amdgcn_s_setprio(3); break;
-    case 1: __builtin_amdgcn_s_setprio(1); break;
-    default: __builtin_amdgcn_s_setprio(0); break;
-    }
-}
-#endif
-
 template <int R, bool WRAPX, bool WRAPY, int NW>
 __device__ __forceinline__ void tile_body_skew(const KArgs &a, int64_t tx, int64_t O, XchS<NW> &xs, int tpar,
-                                               bool prologue, bool first, uint32_t prog0 = 0) {
+                                               bool prologue, bool first) {
     static_assert(R >= 3, "window");
     const int lane = threadIdx.x & 63;
     const int laddr = ((lane - 1) & 63) << 2, raddr = ((lane + 1) & 63) << 2;
@@ -935,17 +892,8 @@ __device__ __forceinline__ void tile_body_skew(const KArgs &a, int64_t tx, int64
         BitEnc::pair_sums(e, o, bperm(laddr, o), bperm(raddr, e), e0, e1, o0, o1);
     };
     const bool last_wave = wi == NW - 1;
-#if LIFE_SKEW_BALANCE
-    const SkewBal bal = skew_bal(a.epoch);
-    uint64_t seen = 0;
-#endif
     for (int g = 1; g <= m; ++g) {
         const int par = g & 1;
-#if LIFE_SKEW_BALANCE
-        skew_prio(bal, seen, prog0 + g);
-        skew_publish(bal, prog0 + g);
-        seen = bal.cu[lane];
-#endif
         // publish the old (generation g-1) last two rows: for the wave below,
         // and from the last wave for the next tile (the ring, this tile's parity)
         xs.x[par][wi][0][lane] = ve[R - 2];
@@ -1064,20 +1012,15 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tskew_bit_kernel(KArg
         // as a segment progresses (the arbiter otherwise favours the oldest
         // waves: the CU's first workgroup finishes first and the last runs
         // its tail alone)
-        if (!LIFE_SKEW_BALANCE) {
-            switch ((int)(4 * (k - k0) / a.seg)) {
-            case 0: __builtin_amdgcn_s_setprio(3); break;
-            case 1: __builtin_amdgcn_s_setprio(2); break;
-            case 2: __builtin_amdgcn_s_setprio(1); break;
-            default: __builtin_amdgcn_s_setprio(0); break;
-            }
+        switch ((int)(4 * (k - k0) / a.seg)) {
+        case 0: __builtin_amdgcn_s_setprio(3); break;
+        case 1: __builtin_amdgcn_s_setprio(2); break;
+        case 2: __builtin_amdgcn_s_setprio(1); break;
+        default: __builtin_amdgcn_s_setprio(0); break;
         }
-        tile_body_skew<R, WRAPX, WRAPY, NW>(a, tx, k * T, xs, tp, false, false, (uint32_t)((k - k0 + 1) * a.m));
+        tile_body_skew<R, WRAPX, WRAPY, NW>(a, tx, k * T, xs, tp, false, false);
         wg_trace((int)(k - k0) + 1);
     }
-#if LIFE_SKEW_BALANCE
-    skew_publish(skew_bal(a.epoch), 0xFFFFFFFFu);  // done: behind nobody
-#endif
 }
 
 template <int R, int GK, bool WRAPX, bool WRAPY, int NW>
@@ -2263,8 +2206,6 @@ hipError_t launch_tskew(const life_layout &Lin, const uint8_t *in, uint8_t *out,
     if (slots == 0) slots = slots_of(fn, 64 * 8);
     const int64_t tiles = a.ntx * a.nty;
     a.seg = slots > 0 ? std::max<int64_t>(1, (tiles + slots - 1) / slots) : 1;
-    static uint32_t epoch = 0;
-    a.epoch = ++epoch;
 
     a.nsc = (a.nty + a.seg - 1) / a.seg;
     const int64_t grid = a.ntx * a.nsc;
