@@ -297,7 +297,8 @@ int life_dev_set_timing(life_dev *d, int on);
  * takes a segment of one tile column top to bottom, a tile's window drifts up
  * one row per generation and takes the two rows above it from the tile
  * before, so no ghost rows are recomputed (m <= 12 generations per launch;
- * 24-row x 8-wave tiles).  Same results. */
+ * 24-row x 8-wave tiles).  Same results; 8 % slower per launch at 65536^2
+ * on MI355X (one round of segments: its tail), hence off. */
 #define LIFE_OPT_SKEW 10
 int life_dev_configure(life_dev *d, int option, int value);
 /* The kernel family that ran the bulk of the last life_dev_step call:
