@@ -702,6 +702,7 @@ __device__ __forceinline__ void tile_body_byte(const TArgs &a, const uint8_t *in
         xch[par][wi][2][lane] = b0;
         xch[par][wi][3][lane] = b1;
         __syncthreads();
+        if (LIFE_WG_TRACE && g == 0) wg_trace(1);  // window loaded, first generation's sums published
         uint32_t a0 = 0u, a1 = 0u, d0 = 0u, d1 = 0u;
         if (wi > 0) {
             a0 = xch[par][wi - 1][2][lane];
@@ -734,6 +735,7 @@ __device__ __forceinline__ void tile_body_byte(const TArgs &a, const uint8_t *in
         v[R - 1] = BitEnc::rule1(p0, p1, b0, b1, d0, d1, bL);
         v[0] = BitEnc::rule1(a0, a1, t0, t1, h10, h11, tL);
     }
+    wg_trace(2);  // generations done
     const int r0 = min(max(K - wi * R, 0), R), r1 = min(max(NW * R - K - wi * R, 0), R);
     const bool st = lane >= 1 && lane <= 62 && j < a.W;
     uint8_t *q = out + (a.ya + y0 + r0) * a.pitch + voff;
@@ -748,6 +750,7 @@ __device__ __forceinline__ void tile_body_byte(const TArgs &a, const uint8_t *in
         }
         q += a.pitch;
     }
+    wg_trace(3);  // stores issued
 }
 
 // Waves per SIMD the bit tiles are compiled for (the VGPR budget): 3 tiles
@@ -1026,6 +1029,7 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tskew_bit_kernel(KArg
 template <int R, int GK, bool WRAPX, bool WRAPY, int NW>
 __global__ __launch_bounds__(64 * NW, LIFE_BYTE_WPE) void tstep_byte_kernel(TArgs a) {
     __shared__ Xch<NW> xch;
+    wg_trace(0);
     int64_t wg = blockIdx.x;
     if (wg < a.xcd_n) {  // per-XCD row-major runs, as tstep_bit_kernel
         const int64_t n = a.xcd_n, x = wg & 7, k = wg >> 3, per = n >> 3, rem = n & 7;

@@ -15,7 +15,8 @@ sys.path.insert(0, os.path.join(ROOT, "mpi-and-open-mp_amd"))
 import life_mi355x as lm  # noqa: E402
 
 gens = int(sys.argv[1]) if len(sys.argv) > 1 else 20
-with lm.Life(65536, 65536, shards=1, kernel="bit") as life:
+kernel = os.environ.get("WG_TRACE_KERNEL", "bit")  # byte: stamps after the load, the generations, the stores
+with lm.Life(65536, 65536, shards=1, kernel=kernel) as life:
     life.fill_random(1, 0.5)
     life.step(5)
     life.step(gens)
@@ -64,7 +65,7 @@ for s_ in np.unique(share):
     m = share == s_
     print(f"  sharing {s_}: {m.sum()} workgroups, median dur {np.median(dur[m]):.1f} us")
 ntile = np.sum(~np.isnan(tiles), axis=1)
-if ntile.max() > 1:  # skewed segments: time per tile (the first includes the prologue)
+if ntile.max() > 1:  # skewed segments: time per tile (the first includes the prologue); byte: per phase
     per = np.diff(np.concatenate([start[:, None], tiles], 1), axis=1)
     print("per tile median by position:", [round(float(np.nanmedian(per[:, k])), 1) for k in range(int(ntile.max()))])
 if len(sys.argv) > 2:
