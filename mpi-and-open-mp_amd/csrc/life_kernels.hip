@@ -638,6 +638,12 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
 #ifndef LIFE_BYTE_LOAD_CHUNK
 #define LIFE_BYTE_LOAD_CHUNK 0
 #endif
+#ifndef LIFE_BYTE_BP_AHEAD
+#define LIFE_BYTE_BP_AHEAD 0
+#endif
+#ifndef LIFE_BYTE_BP_FENCE
+#define LIFE_BYTE_BP_FENCE 1
+#endif
 // Byte tiles: lane l of a tile holds word column 62 tx + l - 1 -- 32 byte
 // cells, packed into one register word per row by v_dot4_u32_u8 on load
 // (two 16-B loads) and unpacked on store -- in the drifting frame
@@ -715,6 +721,13 @@ __device__ __forceinline__ void tile_body_byte(const TArgs &a, const uint8_t *in
         uint32_t p0 = t0, p1 = t1, c0, c1, cL;
         bit_hsum_drift(v[1], laddr, c0, c1, cL);
         const uint32_t h10 = c0, h11 = c1;
+        // LIFE_BYTE_BP_AHEAD rows' left-neighbour words in flight ahead of
+        // their use (0: each fetched in its own row)
+        constexpr int AH = LIFE_BYTE_BP_AHEAD;
+        uint32_t ahead[AH > 0 ? AH : 1];
+#pragma unroll
+        for (int k = 0; k < AH; ++k)
+            if (2 + k < R - 1) ahead[k] = bperm(laddr, v[2 + k]);
 #pragma unroll
         for (int r = 1; r < R - 1; ++r) {
             uint32_t n0, n1, nL;
@@ -722,6 +735,16 @@ __device__ __forceinline__ void tile_body_byte(const TArgs &a, const uint8_t *in
                 n0 = b0;
                 n1 = b1;
                 nL = bL;
+            } else if (AH > 0) {
+                const uint32_t l = ahead[0];
+#pragma unroll
+                for (int k = 0; k + 1 < AH; ++k) ahead[k] = ahead[k + 1];
+                if (r + 1 + AH < R - 1) ahead[AH - 1] = bperm(laddr, v[r + 1 + AH]);
+                // rows stay in program order: the compiler would otherwise
+                // sink every permute next to its use again
+                if (LIFE_BYTE_BP_FENCE) __builtin_amdgcn_sched_barrier(0);
+                nL = __builtin_amdgcn_alignbit(v[r + 1], l, 31);
+                BitEnc::fa(__builtin_amdgcn_alignbit(v[r + 1], l, 30), nL, v[r + 1], n0, n1);
             } else {
                 bit_hsum_drift(v[r + 1], laddr, n0, n1, nL);
             }
