@@ -638,8 +638,14 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
 #ifndef LIFE_BYTE_LOAD_CHUNK
 #define LIFE_BYTE_LOAD_CHUNK 0
 #endif
-#ifndef LIFE_BYTE_BP_AHEAD
-#define LIFE_BYTE_BP_AHEAD 0
+// LIFE_BYTE_BP_AHEAD: the generation loop's left-neighbour permutes are
+// issued this many rows ahead of their use, the rows fenced in program order
+// (LIFE_BYTE_BP_FENCE; unfenced, the compiler sinks every permute next to
+// its use and waits for it).  A tile spends 33 us loading, 93 us in its
+// generations, 4 us storing (scripts/wg_trace.py, profiles/r04/byte_ab):
+// 2 ahead measured 2.29-2.30 against 2.33-2.36 ms per 32-generation launch
+// (4 ahead 2.32, profiles/r04/byte_ab).
+#define LIFE_BYTE_BP_AHEAD 2
 #endif
 #ifndef LIFE_BYTE_BP_FENCE
 #define LIFE_BYTE_BP_FENCE 1
