@@ -645,6 +645,7 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
 // generations, 4 us storing (scripts/wg_trace.py, profiles/r04/byte_ab):
 // 2 ahead measured 2.29-2.30 against 2.33-2.36 ms per 32-generation launch
 // (4 ahead 2.32, profiles/r04/byte_ab).
+#ifndef LIFE_BYTE_BP_AHEAD
 #define LIFE_BYTE_BP_AHEAD 2
 #endif
 #ifndef LIFE_BYTE_BP_FENCE
