@@ -395,6 +395,9 @@ struct XchB {
 #ifndef LIFE_EXP_NO_BARRIER
 #define LIFE_EXP_NO_BARRIER 0
 #endif
+#ifndef LIFE_FAST_WRAP
+#define LIFE_FAST_WRAP 0
+#endif
 #ifndef LIFE_EXP_BPERM_SELF
 #define LIFE_EXP_BPERM_SELF 0
 #endif
@@ -416,8 +419,14 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
     const int64_t j = tx * 62 + pin - 1;                    // pair column of this lane
     int64_t jl;
     if (WRAPX) {
-        jl = j % a.W;
-        if (jl < 0) jl += a.W;
+        // j lies in [-1, W + 62): one conditional add / subtract when W >= 64
+        // (a 64-bit remainder per lane otherwise, ~100 VALU per tile)
+        if (LIFE_FAST_WRAP && a.W >= 64) {
+            jl = j < 0 ? j + a.W : (j >= a.W ? j - a.W : j);
+        } else {
+            jl = j % a.W;
+            if (jl < 0) jl += a.W;
+        }
     } else {
         jl = j > a.W ? a.W : j;  // pairs -1 .. W hold cells / apron; beyond: clamp (never stored)
     }
@@ -432,8 +441,14 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
     {
         int64_t y = y0 + (BAND ? (int64_t)(gl < nb ? gl : nb - 1) * T : 0);  // bands: per-lane rows
         if (WRAPY) {
-            y %= a.h;
-            if (y < 0) y += a.h;
+            // y lies in [-K, h + 64 * T): one conditional add / subtract when
+            // h is at least that margin (a 64-bit remainder otherwise)
+            if (LIFE_FAST_WRAP && a.h >= 64 * (int64_t)(NW * R) + 64) {
+                y = y < 0 ? y + a.h : (y >= a.h ? y - a.h : y);
+            } else {
+                y %= a.h;
+                if (y < 0) y += a.h;
+            }
         }
         const uint8_t *p = row0 + y * a.pitch;
 #pragma unroll
@@ -671,8 +686,12 @@ __device__ __forceinline__ void tile_body_byte(const TArgs &a, const uint8_t *in
     const int64_t j = tx * 62 + lane - 1;  // word column of this lane
     int64_t jl;
     if (WRAPX) {
-        jl = j % a.W;
-        if (jl < 0) jl += a.W;
+        if (LIFE_FAST_WRAP && a.W >= 64) {  // j in [-1, W + 62), as tile_body_bit
+            jl = j < 0 ? j + a.W : (j >= a.W ? j - a.W : j);
+        } else {
+            jl = j % a.W;
+            if (jl < 0) jl += a.W;
+        }
     } else {
         jl = j > a.W ? a.W : j;
     }
@@ -683,8 +702,12 @@ __device__ __forceinline__ void tile_body_byte(const TArgs &a, const uint8_t *in
     {
         int64_t y = y0;
         if (WRAPY) {
-            y %= a.h;
-            if (y < 0) y += a.h;
+            if (LIFE_FAST_WRAP && a.h >= 2 * (int64_t)(NW * R) + 64) {  // y in [-K, h + T)
+                y = y < 0 ? y + a.h : (y >= a.h ? y - a.h : y);
+            } else {
+                y %= a.h;
+                if (y < 0) y += a.h;
+            }
         }
         const uint8_t *p = row0 + y * a.pitch;
 #pragma unroll
