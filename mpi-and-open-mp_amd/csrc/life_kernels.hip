@@ -395,8 +395,14 @@ struct XchB {
 #ifndef LIFE_EXP_NO_BARRIER
 #define LIFE_EXP_NO_BARRIER 0
 #endif
+// LIFE_FAST_WRAP: a tile's wrapped pair column and first row by one
+// conditional add / subtract instead of a 64-bit remainder (per lane for the
+// column) when the axis is long enough for the index to be at most one
+// period out; the remainder stays for short axes.  Driver-shaped launch
+// 0.4346 vs 0.4400 ms mean over three ABAB pairs on one box (-1.2 %, noisy),
+// byte flat; parity + golden modules green (profiles/r04/fastwrap_ad).
 #ifndef LIFE_FAST_WRAP
-#define LIFE_FAST_WRAP 0
+#define LIFE_FAST_WRAP 1
 #endif
 #ifndef LIFE_EXP_BPERM_SELF
 #define LIFE_EXP_BPERM_SELF 0
