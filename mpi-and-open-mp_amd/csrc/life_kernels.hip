@@ -401,9 +401,6 @@ struct XchB {
 // period out; the remainder stays for short axes.  Driver-shaped launch
 // 0.4346 vs 0.4400 ms mean over three ABAB pairs on one box (-1.2 %, noisy),
 // byte flat; parity + golden modules green (profiles/r04/fastwrap_ad).
-#ifndef LIFE_TILE_PRIO
-#define LIFE_TILE_PRIO 0
-#endif
 #ifndef LIFE_FAST_WRAP
 #define LIFE_FAST_WRAP 1
 #endif
@@ -563,15 +560,6 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
 #else
     for (int g = 0; g < a.m; ++g) {
         const int par = g & 1;
-        if (LIFE_TILE_PRIO) {
-            // younger tiles first: issue priority falls as a tile advances,
-            // so the last-dispatched tiles of a launch catch up (its tail)
-            switch (3 * g / a.m) {
-            case 0: __builtin_amdgcn_s_setprio(3); break;
-            case 1: __builtin_amdgcn_s_setprio(2); break;
-            default: __builtin_amdgcn_s_setprio(1); break;
-            }
-        }
         uint32_t pe0, pe1, po0, po1, ce0, ce1, co0, co1;
         {
             uint32_t be0, be1, bo0, bo1;
