@@ -41,10 +41,10 @@ def isa(tmp_path_factory):
     return dis, notes
 
 
-def kernel_lines(dis):
-    """(address, op, text) of every instruction of KERNEL."""
+def kernel_lines(dis, kernel=KERNEL):
+    """(address, op, text) of every instruction of `kernel`."""
     lines = dis.splitlines()
-    start = next(i for i, ln in enumerate(lines) if re.match(r"^[0-9a-f]+ <", ln) and KERNEL in ln)
+    start = next(i for i, ln in enumerate(lines) if re.match(r"^[0-9a-f]+ <", ln) and kernel in ln)
     end = next(i for i in range(start + 1, len(lines)) if re.match(r"^[0-9a-f]+ <.*>:$", lines[i]))
     out = []
     for ln in lines[start + 1:end]:
@@ -99,3 +99,28 @@ def test_vgpr_budget(isa):
     dem = subprocess.run(["c++filt"], input="\n".join(names), capture_output=True, text=True).stdout.splitlines()
     found = [(int(v), int(s)) for n, v, s in zip(dem, vgprs, spills) if KERNEL in n]
     assert found and all(v <= 80 and s == 0 for v, s in found), found
+
+
+BYTE_KERNEL = "tstep_byte_kernel<48, 32, true, true, 8>"  # the 65536^2 byte instance
+
+
+def test_byte_permutes_issued_ahead(isa):
+    """The byte tile's generation loop keeps its left-neighbour permutes two
+    rows ahead of their use (LIFE_BYTE_BP_AHEAD = 2, rows fenced in order;
+    -2 % per launch, profiles/r04/byte_ab): its waits allow two younger LDS
+    operations in flight.  Unfenced, the compiler waits for every permute
+    right after issuing it (lgkmcnt(0) only)."""
+    lines = kernel_lines(isa[0], BYTE_KERNEL)
+    loops = []
+    for addr, op, text in lines:
+        m = re.match(r"s_cbranch_\w+ (\d+)$", text)
+        if not m or int(m.group(1)) < 0x8000:
+            continue
+        target = addr + 4 + 4 * (int(m.group(1)) - 0x10000)
+        body = [t for a, _, t in lines if target <= a <= addr]
+        if any(t.startswith("s_barrier") for t in body) and len(body) > 300:
+            loops.append(body)
+    assert loops, "no byte generation loop found"
+    for body in loops:
+        ahead = sum(1 for t in body if t == "s_waitcnt lgkmcnt(2)")
+        assert ahead >= 40, f"{ahead} waits with two permutes in flight"
