@@ -447,9 +447,10 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
     {
         int64_t y = y0 + (BAND ? (int64_t)(gl < nb ? gl : nb - 1) * T : 0);  // bands: per-lane rows
         if (WRAPY) {
-            // y lies in [-K, h + 64 * T): one conditional add / subtract when
-            // h is at least that margin (a 64-bit remainder otherwise)
-            if (LIFE_FAST_WRAP && a.h >= 64 * (int64_t)(NW * R) + 64) {
+            // y lies in [-K, h + 16 T + NW R) (a band lane adds gl T, gl < 16):
+            // one conditional add / subtract when h exceeds that margin with
+            // room to spare (a 64-bit remainder otherwise)
+            if (LIFE_FAST_WRAP && a.h > 65 * (int64_t)(NW * R)) {
                 y = y < 0 ? y + a.h : (y >= a.h ? y - a.h : y);
             } else {
                 y %= a.h;
