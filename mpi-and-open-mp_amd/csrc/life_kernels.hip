@@ -401,9 +401,6 @@ struct XchB {
 // period out; the remainder stays for short axes.  Driver-shaped launch
 // 0.4346 vs 0.4400 ms mean over three ABAB pairs on one box (-1.2 %, noisy),
 // byte flat; parity + golden modules green (profiles/r04/fastwrap_ad).
-#ifndef LIFE_BIT_BP_AHEAD
-#define LIFE_BIT_BP_AHEAD 0
-#endif
 #ifndef LIFE_FAST_WRAP
 #define LIFE_FAST_WRAP 1
 #endif
@@ -587,17 +584,6 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
             ve[0] = BitEnc::rule1(ae0, ae1, pe0, pe1, ce0, ce1, ve[0]);
             vo[0] = BitEnc::rule1(ao0, ao1, po0, po1, co0, co1, vo[0]);
         }
-        // LIFE_BIT_BP_AHEAD (A/B, default 0 = the compiler's schedule): the
-        // neighbour dwords of that many rows ahead in flight, rows fenced in
-        // program order (as the byte tiles' LIFE_BYTE_BP_AHEAD)
-        constexpr int BAH = LIFE_BIT_BP_AHEAD;
-        uint32_t bl[BAH > 0 ? BAH : 1], br[BAH > 0 ? BAH : 1];
-#pragma unroll
-        for (int k = 0; k < BAH; ++k)
-            if (2 + k < R - 1) {
-                bl[k] = bperm(laddr, vo[2 + k]);
-                br[k] = bperm(raddr, ve[2 + k]);
-            }
 #pragma unroll
         for (int r = 1; r < R - 1; ++r) {
             uint32_t ne0, ne1, no0, no1;
@@ -606,19 +592,6 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
                 ne1 = xch[par][wi + 1][5][lane];
                 no0 = xch[par][wi + 1][6][lane];
                 no1 = xch[par][wi + 1][7][lane];
-            } else if (BAH > 0) {
-                const uint32_t l = bl[0], rr = br[0];
-#pragma unroll
-                for (int k = 0; k + 1 < BAH; ++k) {
-                    bl[k] = bl[k + 1];
-                    br[k] = br[k + 1];
-                }
-                if (r + 1 + BAH < R - 1) {
-                    bl[BAH - 1] = bperm(laddr, vo[r + 1 + BAH]);
-                    br[BAH - 1] = bperm(raddr, ve[r + 1 + BAH]);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                BitEnc::pair_sums(ve[r + 1], vo[r + 1], l, rr, ne0, ne1, no0, no1);
             } else {
                 hsum(ve[r + 1], vo[r + 1], ne0, ne1, no0, no1);
             }
