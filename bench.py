@@ -26,9 +26,12 @@ copies on one MI355X, not yet over xGMI), "cols" column strips.
 N > 1 runs one process per GPU under torch.distributed.run: torch.distributed
 (gloo) carries the bootstrap (RCCL unique id), the barriers and the
 max-over-ranks timing; the halo data path is RCCL ncclSend/ncclRecv issued by
-liblife_mi355x.so itself.  `--gpus N` without a launcher drives N shards from
-one process (one per GPU, ncclCommInitAll; or, with fewer GPUs than shards,
-device-local copies -- how a 1-GPU box rehearses the partitioned schedule).
+liblife_mi355x.so itself.  `--gpus N` without a launcher and with N GPUs
+visible spawns those N rank processes itself (spawn_ranks) before any HIP
+call; `--single-process` instead drives the N GPUs from one process
+(ncclCommInitAll), and with fewer GPUs than shards one process runs them with
+device-local copies (how a 1-GPU box rehearses the partitioned schedule).
+`--shape WxH` replaces --size^2 (the per-GPU blocks of configs[3]).
 Every N > 1 line ends with "phases" (mean ring / interior / halo / block
 times per exchange, from HIP events on the three streams) and
 "parity_vs_1gpu" (the N-shard grid against the same grid run as one shard).
@@ -50,11 +53,7 @@ if int(os.environ.get("WORLD_SIZE", "1")) > 1 or "--rank-mode" in sys.argv:
     # (SONAME libamdhip64.so.7) instead of a second copy from /opt/rocm.
     import torch.distributed  # noqa: F401
 
-import life_mi355x as lm  # noqa: E402
-
-lm._lib()
-
-import numpy as np  # noqa: E402
+import life_mi355x as lm  # noqa: E402  (the module; liblife_mi355x.so loads in main(), after spawn_ranks)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # VALU issue peak: 256 CUs x 4 SIMDs x 32 lanes/cycle (a wave64 instruction
@@ -78,6 +77,9 @@ def parse():
                         "(configs[3])")
     p.add_argument("--size", type=int, default=65536,
                    help="block edge per GPU (weak) or global grid edge (strong)")
+    p.add_argument("--shape", default=None, metavar="WxH",
+                   help="a W x H block per GPU (weak) or global grid (strong) instead of --size^2: the per-GPU "
+                        "blocks of configs[3] are 32768x65536 (N=2), 32768x32768 (N=4), 16384x32768 (N=8)")
     p.add_argument("--workload", default="random", choices=["random", "p46gun_big"])
     p.add_argument("--partition", default=None, choices=["auto", "cart", "rows", "cols"],
                    help="shard shape (life_dims_choose); default: cart (MPI_Dims_create, life_cart.c:117-118: "
@@ -97,6 +99,9 @@ def parse():
     p.add_argument("--no-overlap", action="store_true",
                    help="partitioned shards: every tile in one launch, then the halo exchange (LIFE_OPT_OVERLAP 0) "
                         "instead of ring / interior / halo on three streams")
+    p.add_argument("--single-process", action="store_true",
+                   help="--gpus N > 1 without a launcher: drive the N GPUs from this one process "
+                        "(ncclCommInitAll) instead of spawning one process per GPU")
     p.add_argument("--loopback", action="store_true",
                    help="N = 1: run the single grid as a periodic partition of itself (LIFE_OPT_LOOPBACK): the "
                         "halo exchange, ring / interior overlap and (with --rank-mode) RCCL send/recv of the "
@@ -133,7 +138,7 @@ def cpu_baseline(target_s: float):
                           "gcc -O2, MPICH 3.3.2, mpiexec -n 8 on the build container's 8-core Xeon (not this host)"}}
 
 
-def load_traffic(variant: str, size: int):
+def load_traffic(variant: str, size: str):
     """HBM bytes per stencil launch from the committed rocprofv3 PMC summary
     (scripts/traffic_summary.py); None where not measured for this variant."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
@@ -194,9 +199,85 @@ def parity_vs_1gpu(a, life, grid, nx, ny, gens_done, elapsed, n_gpus, rank, dist
             "reference": {"checksum": want[0], "live": want[1], "shards": 1, "device": 0}}
 
 
+def shape_of(a):
+    """(W, H) of the workload: --shape WxH, else --size^2."""
+    if a.shape:
+        w, h = a.shape.lower().split("x")
+        return int(w), int(h)
+    return a.size, a.size
+
+
+SHAPE_LABELS = {  # the single-GPU blocks the BASELINE configs put on one GPU
+    (32768, 32768): "configs[2]; configs[3]'s N=4 block",
+    (65536, 65536): "configs[4] weak scaling",
+    (32768, 65536): "configs[3]'s N=2 block",
+    (16384, 32768): "configs[3]'s N=8 block",
+}
+
+
+def visible_gpus() -> int:
+    """GPUs this process may use, counted without initialising HIP (on this
+    image torch.cuda.device_count() reads the topology only)."""
+    try:
+        import torch
+
+        return int(torch.cuda.device_count())
+    except Exception:  # noqa: BLE001 -- no torch / no ROCm: no GPUs to spawn for
+        return 0
+
+
+def spawn_ranks(n: int, argv, child=None) -> int:
+    """One process per GPU (3-life/job_life.sh:7-8 runs one MPI rank per core):
+    `bench.py --gpus N` without a launcher starts N children with RANK /
+    WORLD_SIZE / LOCAL_RANK / MASTER_* set, exactly as torch.distributed.run
+    would, and exits with the first failing rank's status.  The parent makes no HIP
+    call before or after (it never loads liblife_mi355x.so); rank 0's JSON line
+    is the one printed.  A single process driving N GPUs serialises ~28
+    runtime calls per shard and exchange pass, more than a
+    strong-scaling device pass."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = child or [sys.executable, os.path.abspath(__file__), *argv]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd, env=env, stdout=None if r == 0 else sys.stderr))
+    rcs = [None] * n
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+        bad = [rc for rc in rcs if rc not in (None, 0)]
+        if bad:  # a dead rank leaves its peers waiting in a collective: stop them (our own children only)
+            first = abs(bad[0])
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    p.terminate()
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    try:
+                        rcs[i] = p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        rcs[i] = p.wait()
+            return first or 1
+        time.sleep(0.05)
+    return 0
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1 and "RANK" not in os.environ and a.gpus > 1 and not a.single_process and not a.rank_mode:
+        if visible_gpus() >= a.gpus:
+            child = os.environ.get("LIFE_BENCH_CHILD_CMD")  # tests: a stand-in for the rank processes
+            sys.exit(spawn_ranks(a.gpus, sys.argv[1:], json.loads(child) if child else None))
+    lm._lib()
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -217,6 +298,8 @@ def main():
     n_gpus = world if world > 1 else a.gpus
     strong = a.scaling == "strong"
     partition = a.partition or "cart"
+    W, H = shape_of(a)
+    shape_txt = f"{W}^2" if W == H else f"{W}x{H}"
     grid = None
     if a.workload == "p46gun_big":
         _, _, grid = lm.load_cfg(os.path.join(ROOT, "tests", "golden", "cfg", "p46gun_big.cfg"))
@@ -225,18 +308,18 @@ def main():
         strong = True
         workload = "p46gun_big.cfg 500x500 (configs[1])"
     elif strong:
-        nx = ny = a.size
+        nx, ny = W, H
         dims = lm.dims_choose(nx, ny, n_gpus, partition)
-        workload = (f"random 50% {a.size}^2 global, {dims[0]}x{dims[1]} blocks over {n_gpus} GPU(s) "
+        workload = (f"random 50% {shape_txt} global, {dims[0]}x{dims[1]} blocks over {n_gpus} GPU(s) "
                     f"(configs[3] strong scaling)")
     else:
-        # weak scaling: the shape is chosen for n_gpus blocks of size^2
-        dims = lm.dims_choose(a.size, a.size * n_gpus, n_gpus, partition)
-        nx, ny = a.size * dims[0], a.size * dims[1]
-        label = {32768: "configs[2]", 65536: "configs[4] weak scaling"}.get(a.size, "weak scaling")
-        if n_gpus == 1 and a.size == 65536:
+        # weak scaling: the shape is chosen for n_gpus blocks of W x H
+        dims = lm.dims_choose(W, H * n_gpus, n_gpus, partition)
+        nx, ny = W * dims[0], H * dims[1]
+        label = SHAPE_LABELS.get((W, H), "weak scaling") if n_gpus == 1 else "configs[4] weak scaling"
+        if n_gpus == 1 and (W, H) == (65536, 65536):
             label = "configs[4] at N=1 = the 65536^2 single-GPU roofline config"
-        workload = f"random 50% {a.size}^2 per GPU, global {nx}x{ny} ({label})"
+        workload = f"random 50% {shape_txt} per GPU, global {nx}x{ny} ({label})"
 
     life = make_life(a, nx, ny, dims, rank_mode, dist, rank, world, local_rank)
     init_grid(life, a, grid)
@@ -322,7 +405,7 @@ def main():
         variant = a.kernel + ("_temporal" if temporal else "_onegen")
         if path == "flow" and a.kernel == "bit":
             variant = "bit_flow"
-        traffic = load_traffic(variant, a.size) if (a.workload == "random" and not strong) else None
+        traffic = load_traffic(variant, shape_txt.replace("^2", "")) if (a.workload == "random" and not strong) else None
         hbm_obj = {"achieved": round(hbm, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                    "frac": round(hbm / HBM_PEAK_GBS, 4),
                    "bytes_per_launch": bytes_per_launch,

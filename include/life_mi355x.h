@@ -289,17 +289,14 @@ int life_dev_set_timing(life_dev *d, int on);
  * when the next pass would outrun it -- the passes in between also advance
  * the apron cells they will read (rows [-e, 0) and [h, h + e), the apron
  * pairs), so one exchange feeds up to K generations instead of one pass of
- * at most LIFE_OPT_BLOCK_GENS.  0: one exchange per pass.  Same results. */
+ * at most LIFE_OPT_BLOCK_GENS.  0: one exchange per pass.  Same results.
+ * Setting it communicates nothing (not a collective; ranks may differ):
+ * part-used aprons are refilled by the next step's first pass that needs
+ * them.  Every life_dev_configure call waits for the device (life_dev_sync). */
 #define LIFE_OPT_DEEP_HALO 9
-/* LIFE_OPT_SKEW (default 0; LIFE_SKEW=1 at load time turns it on): a bit
- * pass over a whole shard (every single-shard pass, the deep-halo passes of a
- * partitioned one) runs as time-skewed parallelogram tiles -- each workgroup
- * takes a segment of one tile column top to bottom, a tile's window drifts up
- * one row per generation and takes the two rows above it from the tile
- * before, so no ghost rows are recomputed (m <= 12 generations per launch;
- * 24-row x 8-wave tiles).  Same results; 8 % slower per launch at 65536^2
- * on MI355X (one round of segments: its tail), hence off. */
-#define LIFE_OPT_SKEW 10
+/* Option 10 (LIFE_OPT_SKEW, time-skewed ghost-free tiles) was retired in
+ * round 5: 8 % slower per launch on MI355X; it now fails
+ * with LIFE_EINVAL like any unknown option. */
 int life_dev_configure(life_dev *d, int option, int value);
 /* The kernel family that ran the bulk of the last life_dev_step call:
  * LIFE_PATH_ONEGEN (one generation per launch), _TILES (temporally blocked
@@ -354,10 +351,9 @@ int life_tune(int kernel, int rows, int depth);
 
 /* Temporal (generations_per_exchange = K > 1) tile height of encoding
  * `kernel` (-1: both, each taking the value if valid for it): register rows
- * per wave -- bit: 16/24/32 rows of 64-cell pairs (default 24), byte:
- * 32/40/48/56/64/96 rows of 32-cell words (default 48); a tile is one
- * workgroup of vertically stacked waves (8; bit: LIFE_TILE_WAVES 8/12/16 at
- * load time for shapes with an instance), waves*rows - 2*ghost owned rows;
+ * per wave -- bit: 16/24 rows of 64-cell pairs (default 24), byte: 32/48
+ * rows of 32-cell words (default 48); a tile is one workgroup of 8
+ * vertically stacked waves, waves*rows - 2*ghost owned rows;
  * 0 keeps the current values; LIFE_TEMPORAL_ROWS / LIFE_TEMPORAL_ROWS_BYTE
  * override at load time. */
 int life_tune_temporal(int kernel, int rows);

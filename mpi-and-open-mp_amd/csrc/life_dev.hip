@@ -142,11 +142,6 @@ static const bool kEnvDeepHalo = [] {
     const char *e = getenv("LIFE_DEEP_HALO");
     return e ? atoi(e) != 0 : true;
 }();
-// LIFE_SKEW (0/1) sets LIFE_OPT_SKEW's default at load time.
-static const bool kEnvSkew = [] {
-    const char *e = getenv("LIFE_SKEW");
-    return e ? atoi(e) != 0 : false;
-}();
 static int default_block_gens(int kernel) {
     return kEnvBlockGens ? kEnvBlockGens : (kernel == LIFE_KERNEL_BIT ? 12 : 32);
 }
@@ -199,7 +194,6 @@ struct life_dev {
     bool loop = false;  // LIFE_OPT_LOOPBACK: the one shard exchanges both axes' halos with itself
     int last_path = LIFE_PATH_NONE;  // life_dev_last_path
     bool deep = kEnvDeepHalo;  // LIFE_OPT_DEEP_HALO: one K-deep exchange feeds several passes
-    bool skew = kEnvSkew;      // LIFE_OPT_SKEW: whole-shard bit passes as skewed (ghost-free) tiles
     int since = 0;  // generations advanced since the aprons were last filled (deep halo)
     int flow = kEnvFlow;  // LIFE_OPT_FLOW: single-shard bit tiles as one persistent dataflow launch per
                           // step call (1: write-through hand-off, 2: plain stores + release; 0 off)
@@ -600,15 +594,8 @@ int launch_tiles(life_dev *d, Shard &s, const life::TileRegion *r, int nreg, int
     const life::Extend xt = ext_;
     const bool ext = ev && (kEnvTimingMode == kTimeExt || kEnvTimingMode == kTimeCall);
     if (ev && !ext) HIPCHK(hipEventRecord(t->a, st));
-    // the whole (extended) shard in one launch: the skewed tiles when enabled
-    const life::TileGeom gw = life::tile_geom(life::extended_layout(s.lay, xt), m);
-    const bool whole = nreg == 1 && r[0].tx0 == 0 && r[0].ty0 == 0 && r[0].tx1 >= gw.ntx && r[0].ty1 >= gw.nty;
-    if (d->skew && whole && life::skew_ok(s.lay, m))
-        HIPCHK(life::launch_tskew(s.lay, in, out, m, wrap_of(d), st, &valu, ext ? t->a : nullptr,
-                                  ext ? t->b : nullptr, xt));
-    else
-        HIPCHK(life::launch_tstep(s.lay, in, out, r, nreg, m, wrap_of(d), st, &valu, ext ? t->a : nullptr,
-                                  ext ? t->b : nullptr, xt));
+    HIPCHK(life::launch_tstep(s.lay, in, out, r, nreg, m, wrap_of(d), st, &valu, ext ? t->a : nullptr,
+                              ext ? t->b : nullptr, xt));
     if (ev && !ext) HIPCHK(hipEventRecord(t->b, st));
     if (d->timing && timed) {
         const life::TileGeom g = life::tile_geom(life::extended_layout(s.lay, xt), m);
@@ -718,7 +705,9 @@ int generation_block(life_dev *d, int m, bool last) {
     // or at the call's end when the next call's first pass could not fit.
     const int K = d->shards[0].lay.generations_per_exchange;
     const bool deep = deep_halo(d);
-    if (deep && d->since + m > K) CHK(exchange(d, 0, false));  // a longer pass than planned for
+    // aprons that no longer cover this pass (a longer pass than planned for,
+    // or the deep halo switched off while they were part-used): refill first
+    if (d->since + m > K) CHK(exchange(d, 0, false));
     const int bmax = std::min(std::min(K, 32), d->block_gens > 0 ? d->block_gens : 32);
     if (deep && d->since + m < K && !(last && d->since + m + bmax > K)) {
         life::Extend xt;
@@ -1621,18 +1610,12 @@ int life_dev_configure(life_dev *d, int option, int value) {
         if (value < 0 || value > 2) return LIFE_EINVAL;
         d->flow = value;
         return LIFE_OK;
-    case LIFE_OPT_SKEW:
-        if (value < 0 || value > 1) return LIFE_EINVAL;
-        d->skew = value != 0;
-        return LIFE_OK;
     case LIFE_OPT_DEEP_HALO:
         if (value < 0 || value > 1) return LIFE_EINVAL;
+        // no communication here: aprons valid only to the
+        // remaining depth K - since are refilled by the next pass that needs
+        // more (generation_block), so the option is local to each rank
         d->deep = value != 0;
-        // aprons that are valid only to the remaining depth: refill them
-        if (d->since > 0) {
-            CHK(exchange(d, 0, false));
-            return life_dev_sync(d);
-        }
         return LIFE_OK;
     case LIFE_OPT_FLOW_CHUNK:
         if (value < 0) return LIFE_EINVAL;
@@ -1757,8 +1740,8 @@ int life_tune(int kernel, int rows, int depth) {
 }
 
 int life_tune_temporal(int kernel, int rows) {
-    const bool bit_ok = rows == 16 || rows == 24 || rows == 32;
-    const bool byte_ok = rows == 32 || rows == 40 || rows == 48 || rows == 56 || rows == 64 || rows == 96;
+    const bool bit_ok = rows == 16 || rows == 24;
+    const bool byte_ok = rows == 32 || rows == 48;
     if (kernel < -1 || kernel > LIFE_KERNEL_BIT) return LIFE_EINVAL;
     if (rows && ((kernel == LIFE_KERNEL_BIT && !bit_ok) || (kernel == LIFE_KERNEL_BYTE && !byte_ok) ||
                  (kernel == -1 && !bit_ok && !byte_ok)))

@@ -110,14 +110,8 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
 // The layout a deep-halo pass tiles: h + 2 ext.y rows starting ext.y rows
 // into the top apron.
 life_layout extended_layout(const life_layout &L, const Extend &ext);
-// Skewed (parallelogram) bit tiles over the whole shard (tskew_bit_kernel):
-// no ghost rows; one launch of m <= 12 generations; 24 x 8 tiles only.
-bool skew_ok(const life_layout &L, int m);
-hipError_t launch_tskew(const life_layout &L, const uint8_t *in, uint8_t *out, int m, Wrap wrap, hipStream_t s,
-                        double *valu_lane_ops = nullptr, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr,
-                        Extend ext = Extend{});
-int temporal_rows(bool bit);      // register rows per wave: bit pair rows 16/24/32, byte word rows 32..96
-int tile_waves(bool bit);         // waves per tile workgroup: bit 8/12/16 (LIFE_TILE_WAVES), byte 8
+int temporal_rows(bool bit);      // register rows per wave: bit pair rows 16/24, byte word rows 32/48
+int tile_waves(bool bit);         // waves per tile workgroup: 8
 // VALU instructions the lanes at one lane position of a tile's waves issue
 // for m generations (the op-count model of life_kernels.hip tstep_kernel,
 // checked against the SQ_INSTS_VALU counter in profiles/); x 64 lanes x tiles.

@@ -23,6 +23,7 @@
 //    2 funnel shifts + 4 ops for the two rows sums, 2 x 8 for the rule).
 #include "life_kernels.h"
 #include "life_bitops.h"
+#include "life_diag.h"
 
 #include <hip/hip_ext.h>
 
@@ -32,28 +33,6 @@
 
 namespace life {
 namespace {
-// LIFE_WG_TRACE (compile time, diagnostics builds only): thread 0 of every
-// workgroup of the bit tile kernels records [start, HW_ID | XCC_ID << 32, end
-// of each tile (up to 14)] (wall clock, 100 MHz) for the last launch;
-// life_debug_wg_trace copies it out.
-#ifndef LIFE_WG_TRACE
-#define LIFE_WG_TRACE 0
-#endif
-#if LIFE_WG_TRACE
-__device__ uint64_t g_wg_trace[16 * 65536];
-__device__ __forceinline__ void wg_trace(int what) {  // 0: start, k >= 1: end of tile k
-    if (threadIdx.x != 0 || blockIdx.x >= 65536 || what > 14) return;
-    uint64_t *t = g_wg_trace + 16 * blockIdx.x;
-    t[what == 0 ? 0 : what + 1] = wall_clock64();
-    if (what == 0) {
-        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-        const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);
-        t[1] = (uint64_t)hw | ((uint64_t)xcc << 32);
-    }
-}
-#else
-__device__ __forceinline__ void wg_trace(int) {}
-#endif
 
 constexpr int kBlock = 256;  // 4 waves of 64
 
@@ -340,21 +319,9 @@ using Xch = uint32_t[2][NW][4][64];  // byte tiles: [parity][wave][top s0/s1, bo
 // wave index in the generation loop
 template <int NW>
 using XchP = uint32_t[2][NW + 2][8][64];
-// LIFE_BIT_REORDER (compile time, default 0): the generation loop publishes
-// its edge rows' sums, updates the interior rows, and only then meets the
-// barrier and updates rows 0 and R-1 -- the LDS writes drain while the
-// interior computes instead of right before the barrier.  Row 1's sums wait
-// in a wave-private LDS slot (XchB::priv; 8 KB per 8-wave tile) rather than
-// in 4 more VGPRs.
-#ifndef LIFE_BIT_REORDER
-#define LIFE_BIT_REORDER 0
-#endif
 template <int NW>
 struct XchB {
     XchP<NW> s;
-#if LIFE_BIT_REORDER
-    uint32_t priv[NW][4][64];
-#endif
 };
 
 // Bit tiles over interleaved pairs.  Lane l of a tile holds pair column
@@ -386,15 +353,6 @@ struct XchB {
 // read beyond the tile, absorbed by the ghost lanes.  Only the loads and
 // stores differ (per-lane rows); the generation loop is the tile's.  gsh = 6:
 // an ordinary tile (nb = 1).
-// Timing-only experiment switches (scripts/build_variants.sh; results are
-// WRONG with either set, the parity tests do not apply): LIFE_EXP_NO_BARRIER
-// drops the per-generation workgroup barrier, LIFE_EXP_BPERM_SELF makes the
-// two neighbour fetches return the lane's own dwords (no LDS permute).
-// Together with SQ_WAIT_* they bound the barrier and the permute latency
-// separately.
-#ifndef LIFE_EXP_NO_BARRIER
-#define LIFE_EXP_NO_BARRIER 0
-#endif
 // LIFE_FAST_WRAP: a tile's wrapped pair column and first row by one
 // conditional add / subtract instead of a 64-bit remainder (per lane for the
 // column) when the axis is long enough for the index to be at most one
@@ -403,9 +361,6 @@ struct XchB {
 // byte flat; parity + golden modules green (profiles/r04/fastwrap_ad).
 #ifndef LIFE_FAST_WRAP
 #define LIFE_FAST_WRAP 1
-#endif
-#ifndef LIFE_EXP_BPERM_SELF
-#define LIFE_EXP_BPERM_SELF 0
 #endif
 
 template <int R, bool WRAPX, bool WRAPY, int FLOW, int NW, bool BAND = false>
@@ -478,10 +433,7 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
         }
     }
     auto hsum = [&](uint32_t e, uint32_t o, uint32_t &e0, uint32_t &e1, uint32_t &o0, uint32_t &o1) {
-        if (LIFE_EXP_BPERM_SELF)
-            BitEnc::pair_sums(e, o, o, e, e0, e1, o0, o1);
-        else
-            BitEnc::pair_sums(e, o, bperm(laddr, o), bperm(raddr, e), e0, e1, o0, o1);
+        BitEnc::pair_sums(e, o, bperm(laddr, o), bperm(raddr, e), e0, e1, o0, o1);
     };
     // Register budget (80 VGPRs at 3 tiles per CU, R = 24: 48 hold the
     // window): only the rolling sums of three rows stay live across the
@@ -494,71 +446,6 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
     // spilling (46-83 VGPRs at R = 24).
     if (wi == 0 || wi == NW - 1)  // the dead slots (ordered by the first barrier below)
         for (int q = 0; q < 16; ++q) xch[q >> 3][wi == 0 ? 0 : NW + 1][q & 7][lane] = 0u;
-#if LIFE_BIT_REORDER
-    for (int g = 0; g < a.m; ++g) {
-        const int par = g & 1;
-        uint32_t pe0, pe1, po0, po1, ce0, ce1, co0, co1;
-        {
-            uint32_t e0, e1, o0, o1;
-            hsum(ve[R - 1], vo[R - 1], e0, e1, o0, o1);
-            xch[par][wi + 1][4][lane] = e0;
-            xch[par][wi + 1][5][lane] = e1;
-            xch[par][wi + 1][6][lane] = o0;
-            xch[par][wi + 1][7][lane] = o1;
-        }
-        hsum(ve[0], vo[0], pe0, pe1, po0, po1);
-        xch[par][wi + 1][0][lane] = pe0;
-        xch[par][wi + 1][1][lane] = pe1;
-        xch[par][wi + 1][2][lane] = po0;
-        xch[par][wi + 1][3][lane] = po1;
-        hsum(ve[1], vo[1], ce0, ce1, co0, co1);
-        xb.priv[wi][0][lane] = ce0;
-        xb.priv[wi][1][lane] = ce1;
-        xb.priv[wi][2][lane] = co0;
-        xb.priv[wi][3][lane] = co1;
-#pragma unroll
-        for (int r = 1; r < R - 1; ++r) {
-            uint32_t ne0, ne1, no0, no1;
-            if (r + 1 == R - 1) {  // this wave's own bottom sums, published above
-                ne0 = xch[par][wi + 1][4][lane];
-                ne1 = xch[par][wi + 1][5][lane];
-                no0 = xch[par][wi + 1][6][lane];
-                no1 = xch[par][wi + 1][7][lane];
-            } else {
-                hsum(ve[r + 1], vo[r + 1], ne0, ne1, no0, no1);
-            }
-            ve[r] = BitEnc::rule1(pe0, pe1, ce0, ce1, ne0, ne1, ve[r]);
-            vo[r] = BitEnc::rule1(po0, po1, co0, co1, no0, no1, vo[r]);
-            pe0 = ce0;
-            pe1 = ce1;
-            po0 = co0;
-            po1 = co1;
-            ce0 = ne0;
-            ce1 = ne1;
-            co0 = no0;
-            co1 = no1;
-        }
-        if (!LIFE_EXP_NO_BARRIER) __syncthreads();
-        {
-            // row R-1: the old rows R-2 (p) and R-1 (c) and the wave below
-            const uint32_t de0 = xch[par][wi + 2][0][lane], de1 = xch[par][wi + 2][1][lane];
-            const uint32_t do0 = xch[par][wi + 2][2][lane], do1 = xch[par][wi + 2][3][lane];
-            ve[R - 1] = BitEnc::rule1(pe0, pe1, ce0, ce1, de0, de1, ve[R - 1]);
-            vo[R - 1] = BitEnc::rule1(po0, po1, co0, co1, do0, do1, vo[R - 1]);
-        }
-        {
-            // row 0: the wave above and this wave's old rows 0 and 1
-            const uint32_t ae0 = xch[par][wi][4][lane], ae1 = xch[par][wi][5][lane];
-            const uint32_t ao0 = xch[par][wi][6][lane], ao1 = xch[par][wi][7][lane];
-            const uint32_t te0 = xch[par][wi + 1][0][lane], te1 = xch[par][wi + 1][1][lane];
-            const uint32_t to0 = xch[par][wi + 1][2][lane], to1 = xch[par][wi + 1][3][lane];
-            const uint32_t se0 = xb.priv[wi][0][lane], se1 = xb.priv[wi][1][lane];
-            const uint32_t so0 = xb.priv[wi][2][lane], so1 = xb.priv[wi][3][lane];
-            ve[0] = BitEnc::rule1(ae0, ae1, te0, te1, se0, se1, ve[0]);
-            vo[0] = BitEnc::rule1(ao0, ao1, to0, to1, so0, so1, vo[0]);
-        }
-    }
-#else
     for (int g = 0; g < a.m; ++g) {
         const int par = g & 1;
         uint32_t pe0, pe1, po0, po1, ce0, ce1, co0, co1;
@@ -575,7 +462,7 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
         xch[par][wi + 1][1][lane] = pe1;
         xch[par][wi + 1][2][lane] = po0;
         xch[par][wi + 1][3][lane] = po1;
-        if (!LIFE_EXP_NO_BARRIER) __syncthreads();
+        __syncthreads();
         hsum(ve[1], vo[1], ce0, ce1, co0, co1);
         {
             // the wave above (slot 0 above the window: zero, dead ghost rows)
@@ -614,7 +501,6 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
             vo[R - 1] = BitEnc::rule1(po0, po1, co0, co1, do0, do1, vo[R - 1]);
         }
     }
-#endif
     // window rows [K, NW*R - K) are the tile's owned rows [ty*T, ty*T + T);
     // this wave's share of them (a half-height tile's ghost rows may span more
     // than one wave: K > R)
@@ -745,7 +631,7 @@ __device__ __forceinline__ void tile_body_byte(const TArgs &a, const uint8_t *in
         xch[par][wi][2][lane] = b0;
         xch[par][wi][3][lane] = b1;
         __syncthreads();
-        if (LIFE_WG_TRACE && g == 0) wg_trace(1);  // window loaded, first generation's sums published
+        if (g == 0) wg_trace(1);  // window loaded, first generation's sums published
         uint32_t a0 = 0u, a1 = 0u, d0 = 0u, d1 = 0u;
         if (wi > 0) {
             a0 = xch[par][wi - 1][2][lane];
@@ -856,234 +742,6 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tstep_bit_kernel(TArg
         tile_body_bit<R, WRAPX, WRAPY, 0, NW, true>(a, a.in, a.out, a.bcol, ty, xch, a.gsh, nb);
     }
     wg_trace(1);
-}
-
-// ------------------------------------------------------------------ skewed bit tiles
-// Parallelogram (time-skewed) tiles: no ghost rows.  A tile of NW waves x R
-// pair rows computes, at generation g, the domain rows [O + m - g, O + m - g
-// + NW*R): its window drifts up one row per generation, so every row's new
-// value reads the row itself and the two rows ABOVE it in register order
-// (new_i = rule(h(old_{i-2}), h(old_{i-1}), h(old_i), alive = old_{i-1})) and
-// nothing below.  The two rows above wave 0 come from the tile above at the
-// same generation, which the same workgroup ran just before (a segment of S
-// consecutive tiles of one tile column per workgroup, top to bottom), through
-// an LDS ring of one entry per generation; a segment's first tile takes them
-// from a 24-row prologue window (8 waves x 3 rows, its own top fed zeros:
-// the wrong values it starts with spread two rows per generation in window
-// terms and never reach its bottom two rows within m <= 12 generations).
-// After m generations register row i of wave w holds domain row O + wR + i:
-// tiles of 192 rows partition the domain, read it once (+ 24 prologue rows
-// per segment) and recompute nothing but the two rows above each wave (12
-// VALU per wave and generation, 2.3 %) -- where tile_body_bit recomputes 2m
-// ghost rows per 192-row window (10.4 % at m = 10).
-//
-// LDS: the inter-wave exchange holds the raw (E, O) of each wave's last two
-// rows per generation parity (16 KB at 8 waves), the ring the same four
-// dwords per generation for two tiles (tile parity: 24 KB): 40 KB, 3
-// workgroups per CU, as the per-launch tiles.
-//
-// Measured (65536^2, driver-shaped call; DESIGN.md 5.1, profiles/r04/k-t):
-// parity green, but 0.450 ms per launch against 0.416 for tile_body_bit.
-// With all three workgroups of a CU resident a skewed tile costs 5 % less
-// per owned row than a per-launch tile (16.5 vs 15.6 us per tile per CU,
-// 192 vs 172 owned rows); what it loses is the tail: one workgroup per
-// segment means one round of 731 workgroups, the CU's oldest workgroup
-// issues first and finishes first, and the last third of the launch runs
-// with one or two workgroups per CU (scripts/wg_trace.py).  Opt-in
-// (LIFE_OPT_SKEW / LIFE_SKEW=1).  The three measured fixes kept below: the
-// barrier pinned after the publish with the rows above read right after it
-// (the compiler otherwise sank it to the sweep's end: 0.50 -> 0.48 ms),
-// segments dealt XCD-aware (HBM fetch 1.23x -> 1.02x of the per-launch
-// tiles'), issue priority falling along a segment (0.48 -> 0.45 ms).
-struct KArgs {
-    const uint8_t *in;
-    uint8_t *out;
-    int64_t pitch, xoff, W, h, ya;  // domain: rows [0, h) start at buffer row ya; W pairs per row
-    int64_t ylo;                    // lowest readable domain row (non-wrapped y: -ya)
-    int64_t ntx, nty, seg, nsc;     // tile columns, tiles per column, tiles per segment, segments per column
-    int32_t m, xext;
-};
-template <int NW>
-struct XchS {
-    uint32_t x[2][NW][4][64];     // [gen parity][wave][E(R-2), O(R-2), E(R-1), O(R-1)][lane]
-    uint32_t ring[2][12][4][64];  // [tile parity][generation - 1][same][lane]
-};
-
-template <int R, bool WRAPX, bool WRAPY, int NW>
-__device__ __forceinline__ void tile_body_skew(const KArgs &a, int64_t tx, int64_t O, XchS<NW> &xs, int tpar,
-                                               bool prologue, bool first) {
-    static_assert(R >= 3, "window");
-    const int lane = threadIdx.x & 63;
-    const int laddr = ((lane - 1) & 63) << 2, raddr = ((lane + 1) & 63) << 2;
-    const int wi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int m = a.m;
-    const int64_t j = tx * 62 + lane - 1;  // pair column of this lane
-    int64_t jl;
-    if (WRAPX) {
-        jl = j % a.W;
-        if (jl < 0) jl += a.W;
-    } else {
-        jl = j > a.W ? a.W : j;
-    }
-    const uint32_t voff = (uint32_t)(a.xoff + 8 * jl);
-    // generation-0 domain row of register row 0 (the prologue: the NW*R rows
-    // above the tile's first input row)
-    const int64_t y0 = O + m + (int64_t)wi * R - (prologue ? (int64_t)NW * R : 0);
-    const uint8_t *row0 = a.in + a.ya * a.pitch;
-    uint32_t ve[R], vo[R];
-    {
-        // one wave-uniform row per register row, walked (no division per
-        // row): wrapped, or clamped to the readable rows (only a prologue's
-        // top reaches above them, and those rows lie outside the cone of
-        // every value it hands on)
-        int64_t y = y0;
-        if (WRAPY) {
-            y %= a.h;
-            if (y < 0) y += a.h;
-        }
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int64_t yy = (!WRAPY && y < a.ylo) ? a.ylo : y;
-            const uint64_t q = *reinterpret_cast<const uint64_t *>(row0 + yy * a.pitch + voff);
-            ve[r] = (uint32_t)q;
-            vo[r] = (uint32_t)(q >> 32);
-            ++y;
-            if (WRAPY && y == a.h) y = 0;
-        }
-    }
-    auto hsum = [&](uint32_t e, uint32_t o, uint32_t &e0, uint32_t &e1, uint32_t &o0, uint32_t &o1) {
-        BitEnc::pair_sums(e, o, bperm(laddr, o), bperm(raddr, e), e0, e1, o0, o1);
-    };
-    const bool last_wave = wi == NW - 1;
-    for (int g = 1; g <= m; ++g) {
-        const int par = g & 1;
-        // publish the old (generation g-1) last two rows: for the wave below,
-        // and from the last wave for the next tile (the ring, this tile's parity)
-        xs.x[par][wi][0][lane] = ve[R - 2];
-        xs.x[par][wi][1][lane] = vo[R - 2];
-        xs.x[par][wi][2][lane] = ve[R - 1];
-        xs.x[par][wi][3][lane] = vo[R - 1];
-        {
-            // (the other waves write their exchange slot a second time: no
-            // branch, no extra LDS)
-            uint32_t(*dst)[64] = last_wave ? xs.ring[tpar][g - 1] : xs.x[par][wi];
-            dst[0][lane] = ve[R - 2];
-            dst[1][lane] = vo[R - 2];
-            dst[2][lane] = ve[R - 1];
-            dst[3][lane] = vo[R - 1];
-        }
-        // one barrier per generation, right after publishing (as the
-        // per-launch tiles): the reads of the rows above come at the sweep's
-        // end, their latency hidden behind it
-        __syncthreads();
-        // the two rows above: the wave above, or (wave 0) the tile above
-        // through the ring, or (a prologue's wave 0) zeros
-        // (a uniform pointer select and mask: no branch in the loop body)
-        // (read here, with their neighbour dwords, and used at the sweep's
-        // end; the scheduling fence keeps the compiler from sinking the
-        // barrier to the sweep's end)
-        const uint32_t(*src)[64] = wi > 0 ? xs.x[par][wi > 0 ? wi - 1 : 0] : xs.ring[tpar ^ 1][g - 1];
-        const uint32_t keep = (first && wi == 0) ? 0u : ~0u;
-        const uint32_t pe2 = src[0][lane] & keep, po2 = src[1][lane] & keep;
-        const uint32_t pe1 = src[2][lane] & keep, po1 = src[3][lane] & keep;
-        const uint32_t pl1 = bperm(laddr, po1), pr1 = bperm(raddr, pe1);
-        const uint32_t pl2 = bperm(laddr, po2), pr2 = bperm(raddr, pe2);
-        __builtin_amdgcn_sched_barrier(0);
-        // rows R-1 .. 2, bottom up: new_i = rule(h_{i-2}, h_{i-1}, h_i, old_{i-1})
-        uint32_t ae0, ae1, ao0, ao1;  // h_{i-2}
-        uint32_t be0, be1, bo0, bo1;  // h_{i-1}
-        uint32_t ce0, ce1, co0, co1;  // h_i
-        hsum(ve[R - 1], vo[R - 1], ce0, ce1, co0, co1);
-        hsum(ve[R - 2], vo[R - 2], be0, be1, bo0, bo1);
-        // the neighbour dwords of the next row are fetched one step ahead
-        uint32_t nl = bperm(laddr, vo[R - 3]), nr = bperm(raddr, ve[R - 3]);
-#pragma unroll
-        for (int i = R - 1; i >= 2; --i) {
-            const uint32_t cl = nl, cr = nr;
-            if (i >= 3) {
-                nl = bperm(laddr, vo[i - 3]);
-                nr = bperm(raddr, ve[i - 3]);
-            }
-            BitEnc::pair_sums(ve[i - 2], vo[i - 2], cl, cr, ae0, ae1, ao0, ao1);
-            ve[i] = BitEnc::rule1(ae0, ae1, be0, be1, ce0, ce1, ve[i - 1]);
-            vo[i] = BitEnc::rule1(ao0, ao1, bo0, bo1, co0, co1, vo[i - 1]);
-            ce0 = be0;
-            ce1 = be1;
-            co0 = bo0;
-            co1 = bo1;
-            be0 = ae0;
-            be1 = ae1;
-            bo0 = ao0;
-            bo1 = ao1;
-        }
-        // now b = h_0, c = h_1
-        uint32_t me0, me1, mo0, mo1;  // h_{-1}
-        BitEnc::pair_sums(pe1, po1, pl1, pr1, me0, me1, mo0, mo1);
-        // row 1: rule(h_{-1}, h_0, h_1, old_0)
-        ve[1] = BitEnc::rule1(me0, me1, be0, be1, ce0, ce1, ve[0]);
-        vo[1] = BitEnc::rule1(mo0, mo1, bo0, bo1, co0, co1, vo[0]);
-        BitEnc::pair_sums(pe2, po2, pl2, pr2, ae0, ae1, ao0, ao1);  // h_{-2}
-        // row 0: rule(h_{-2}, h_{-1}, h_0, old_{-1})
-        ve[0] = BitEnc::rule1(ae0, ae1, me0, me1, be0, be1, pe1);
-        vo[0] = BitEnc::rule1(ao0, ao1, mo0, mo1, bo0, bo1, po1);
-    }
-    __syncthreads();  // the exchange slots and the ring are reused by the next tile
-    if (prologue) return;
-    // register row i of wave wi now holds domain row O + wi*R + i
-    int lane2 = (int)(threadIdx.x & 63);
-    asm volatile("" : "+v"(lane2));
-    const int64_t j2 = tx * 62 + lane2 - 1;
-    const bool st = (lane2 >= 1 && lane2 <= 62 && j2 < a.W) || (!WRAPX && a.xext && (j2 == -1 || j2 == a.W));
-    int64_t jl2;  // the load's column again: only the window lives across the loop
-    if (WRAPX) {
-        jl2 = j2 % a.W;
-        if (jl2 < 0) jl2 += a.W;
-    } else {
-        jl2 = j2 > a.W ? a.W : j2;
-    }
-    const int64_t yb = O + (int64_t)wi * R;
-    uint8_t *q = a.out + (a.ya + yb) * a.pitch + (uint32_t)(a.xoff + 8 * jl2);
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        if (st && yb + r < a.h) *reinterpret_cast<uint64_t *>(q) = (uint64_t)ve[r] | ((uint64_t)vo[r] << 32);
-        q += a.pitch;
-    }
-}
-
-// One workgroup per segment: a prologue, then its tiles top to bottom.
-template <int R, bool WRAPX, bool WRAPY, int NW>
-__global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tskew_bit_kernel(KArgs a) {
-    __shared__ XchS<NW> xs;
-    wg_trace(0);
-    int64_t b = blockIdx.x;
-    {
-        // the dispatcher deals blocks round-robin over the 8 XCDs: XCD x runs
-        // blocks 8k + x, here segments first_x + k, so a segment row's tile
-        // columns share one L2 (each 512-B row piece straddles the 128-B
-        // lines it shares with the next column: fetched once, not twice)
-        const int64_t n = a.ntx * a.nsc, x = b & 7, k = b >> 3, per = n >> 3, rem = n & 7;
-        b = (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + k;
-    }
-    const int64_t sc = b / a.ntx, tx = b % a.ntx;
-    const int64_t k0 = sc * a.seg, k1 = k0 + a.seg < a.nty ? k0 + a.seg : a.nty;
-    if (k0 >= k1) return;  // whole workgroup
-    const int64_t T = (int64_t)NW * R;
-    tile_body_skew<3, WRAPX, WRAPY, NW>(a, tx, k0 * T, xs, 0, true, true);
-    int tp = 1;
-    for (int64_t k = k0; k < k1; ++k, tp ^= 1) {
-        // the workgroups sharing a CU advance together: issue priority falls
-        // as a segment progresses (the arbiter otherwise favours the oldest
-        // waves: the CU's first workgroup finishes first and the last runs
-        // its tail alone)
-        switch ((int)(4 * (k - k0) / a.seg)) {
-        case 0: __builtin_amdgcn_s_setprio(3); break;
-        case 1: __builtin_amdgcn_s_setprio(2); break;
-        case 2: __builtin_amdgcn_s_setprio(1); break;
-        default: __builtin_amdgcn_s_setprio(0); break;
-        }
-        tile_body_skew<R, WRAPX, WRAPY, NW>(a, tx, k * T, xs, tp, false, false);
-        wg_trace((int)(k - k0) + 1);
-    }
 }
 
 template <int R, int GK, bool WRAPX, bool WRAPY, int NW>
@@ -1855,14 +1513,13 @@ Tunings &tunings() {
     static Tunings t;
     return t;
 }
-bool temporal_rows_ok(bool bit, int nr) {
-    return bit ? (nr == 16 || nr == 24 || nr == 32)
-               : (nr == 32 || nr == 40 || nr == 48 || nr == 56 || nr == 64 || nr == 96);
-}
+// Tile heights with a kernel instance.  Round 5 kept the shipped shapes and
+// one alternative each: every other shape measured slower at 65536^2
+// (profiles/r02/r2w, r03/r4g) and at 32768^2 (bit 32x8, 24x12, 16x16:
+// 0.96-0.99 of 24x8, profiles/r05/a).
+bool temporal_rows_ok(bool bit, int nr) { return bit ? (nr == 16 || nr == 24) : (nr == 32 || nr == 48); }
 // bit tile shapes with a kernel instance (pair rows R x waves NW)
-bool bit_shape_ok(int R, int NW) {
-    return (NW == 8 && (R == 16 || R == 24 || R == 32)) || (NW == 12 && R == 24) || (NW == 16 && (R == 16 || R == 24));
-}
+bool bit_shape_ok(int R, int NW) { return NW == 8 && (R == 16 || R == 24); }
 }  // namespace
 
 StepTuning step_tuning(bool bit) { return tunings().t[bit ? 1 : 0]; }
@@ -1997,10 +1654,6 @@ template <int GK>
 const void *byte_k(Wrap wrap) {
     switch (temporal_rows(false)) {
     case 32: return byte_fn<32, GK>(wrap);
-    case 40: return byte_fn<40, GK>(wrap);
-    case 56: return byte_fn<56, GK>(wrap);
-    case 64: return byte_fn<64, GK>(wrap);
-    case 96: return byte_fn<96, GK>(wrap);
     default: return byte_fn<48, GK>(wrap);
     }
 }
@@ -2014,7 +1667,7 @@ const void *bit_fn(Wrap wrap) {
 }
 
 // the bit tile shape's instances: per-launch tiles and the occupancy probe
-#define LIFE_BIT_SHAPES(X) X(24, 8) X(16, 8) X(32, 8) X(24, 12) X(16, 16) X(24, 16)
+#define LIFE_BIT_SHAPES(X) X(24, 8) X(16, 8)
 const void *bit_k(Wrap wrap) {
     const int R = temporal_rows(true), NW = tile_waves(true);
 #define LIFE_BIT_CASE(r, nw) \
@@ -2224,58 +1877,6 @@ hipError_t launch_tstep(const life_layout &Lin, const uint8_t *in, uint8_t *out,
                                             : byte_k<32>(wrap);
     if (!fn) return hipErrorInvalidValue;
     return launch_fn(fn, (unsigned)items, 64u * (unsigned)tile_waves(bit), &a, s, ev0, ev1);
-}
-
-// Skewed bit tiles (tskew_bit_kernel): the 24 x 8 shape only.
-namespace {
-const void *skew_fn(Wrap wrap) {
-    if (wrap.x && wrap.y) return (const void *)tskew_bit_kernel<24, true, true, 8>;
-    if (wrap.x) return (const void *)tskew_bit_kernel<24, true, false, 8>;
-    if (wrap.y) return (const void *)tskew_bit_kernel<24, false, true, 8>;
-    return (const void *)tskew_bit_kernel<24, false, false, 8>;
-}
-}  // namespace
-
-bool skew_ok(const life_layout &L, int m) {
-    return is_bit(L) && L.generations_per_exchange > 1 && m >= 1 && m <= 12 && temporal_rows(true) == 24 &&
-           tile_waves(true) == 8;
-}
-
-hipError_t launch_tskew(const life_layout &Lin, const uint8_t *in, uint8_t *out, int m, Wrap wrap, hipStream_t s,
-                        double *valu_lane_ops, hipEvent_t ev0, hipEvent_t ev1, Extend ext) {
-    const int K = Lin.generations_per_exchange;
-    if (!skew_ok(Lin, m) || m > K || Lin.yapron != K || ext.y < 0 || ext.y + m > K ||
-        (ext.y > 0 && wrap.y) || (ext.x && wrap.x))
-        return hipErrorInvalidValue;
-    const life_layout L = extended_layout(Lin, ext);
-    constexpr int64_t T = 24 * 8;  // rows per tile
-    KArgs a;
-    a.in = in;
-    a.out = out;
-    a.pitch = L.pitch;
-    a.xoff = L.xoff;
-    a.W = (L.w + 63) / 64;
-    a.h = L.h;
-    a.ya = L.yapron;
-    a.ylo = -L.yapron;
-    a.ntx = (a.W + 61) / 62;
-    a.nty = (L.h + T - 1) / T;
-    a.m = m;
-    a.xext = ext.x ? 1 : 0;
-    // one round of resident workgroups: each takes a segment of seg
-    // consecutive tiles of one column (one prologue per segment)
-    const void *fn = skew_fn(wrap);
-    static int cached[4] = {0, 0, 0, 0};
-    int &slots = cached[(wrap.x ? 2 : 0) + (wrap.y ? 1 : 0)];
-    if (slots == 0) slots = slots_of(fn, 64 * 8);
-    const int64_t tiles = a.ntx * a.nty;
-    a.seg = slots > 0 ? std::max<int64_t>(1, (tiles + slots - 1) / slots) : 1;
-
-    a.nsc = (a.nty + a.seg - 1) / a.seg;
-    const int64_t grid = a.ntx * a.nsc;
-    if (valu_lane_ops)  // per lane and generation: 24 rows x 22 + 12 (the two rows above), prologue 3 x 22 + 12
-        *valu_lane_ops = 64.0 * 8.0 * (double)m * ((double)tiles * (24.0 * 22.0 + 12.0) + (double)grid * (3.0 * 22.0 + 12.0));
-    return launch_fn(fn, (unsigned)grid, 64u * 8u, &a, s, ev0, ev1);
 }
 
 namespace {
@@ -2570,14 +2171,3 @@ hipError_t launch_census(const life_layout &L, int64_t nx, const uint8_t *buf, u
 }
 
 }  // namespace life
-
-#if LIFE_WG_TRACE
-// Diagnostics builds only: the per-workgroup trace of the last bit tile launch.
-extern "C" int life_debug_wg_trace(uint64_t *host, int64_t n) {
-    if (n > 16 * 65536) n = 16 * 65536;
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(life::g_wg_trace), n * sizeof(uint64_t), 0, hipMemcpyDeviceToHost) ==
-                   hipSuccess
-               ? 0
-               : -1;
-}
-#endif

@@ -44,7 +44,6 @@ HALO_COLUMN, HALO_ROW = 0, 1
 OPT_SMALL_GRID, OPT_OVERLAP, OPT_SMALL_WINDOW, OPT_BLOCK_GENS, OPT_LOOPBACK, OPT_FLOW = 1, 2, 4, 5, 6, 7
 OPT_FLOW_CHUNK = 8
 OPT_DEEP_HALO = 9
-OPT_SKEW = 10
 # LIFE_TEMPORAL_DEPTH(_BYTE): generations per halo exchange of the temporal layouts
 TEMPORAL_DEPTH = {"bit": 32, "byte": 32}
 BLOCK_GENS = {"bit": 12, "byte": 32}  # tiles: default generations per launch at most (LIFE_OPT_BLOCK_GENS)
@@ -239,7 +238,7 @@ def density_to_thr(density: float) -> int:
 
 def tune_temporal(rows: int = 0, kernel=-1) -> None:
     """Temporal tile height: register rows per wave of one encoding (bit:
-    16/24/32 pair rows; byte: 32/40/48/56/64/96 word rows), or of both
+    16/24 pair rows; byte: 32/48 word rows), or of both
     (kernel -1: each takes the value if valid for it)."""
     _check(_lib().life_tune_temporal(kernel_id(kernel), rows), "life_tune_temporal")
 

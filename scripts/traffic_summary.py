@@ -12,10 +12,11 @@ MI355X_MICROARCH.md's HBM section prescribes for gfx950:
 * the temporal bit kernel loads and stores 4 B per lane (natural-word tiles,
   rounds 1-2) or 8 B per lane (interleaved-pair tiles, tstep_bit_kernel,
   round 3), access widths the guide lists as uncalibrated:
-  scripts/calib_4b.hip / calib_8b.hip copy 1 GiB with 4-B / 8-B lanes and
-  read FETCH_SIZE = 0.500 GiB, WRITE_SIZE = 1.000 GiB
-  (profiles/r01/calib_4b_*.csv, profiles/r03/calib_8b_*.csv), so the same
-  x2 / x1 applies.
+  copies of 1 GiB with 4-B / 8-B lanes read FETCH_SIZE = 0.500 GiB,
+  WRITE_SIZE = 1.000 GiB (profiles/r01/calib_4b_*.csv, recorded by the
+  4-B calibration kernel retired in round 4 -- in git history before
+  commit 31896c8; profiles/r03/calib_8b_*.csv from scripts/calib_8b.hip), so
+  the same x2 / x1 applies.
 
 Only full-length launches are summarised (the median over the dispatches of
 the dominant kernel).
@@ -66,7 +67,8 @@ for var, (needle, calibrated) in VARIANTS.items():
         out[key + "_detail"] = {"fetch_bytes_corrected": round(fetch), "fetch_size_raw_bytes": round(vals["FETCH_SIZE"]),
                                 "write_bytes": round(vals["WRITE_SIZE"]), "source": f"profiles/{rnd}/pmc_*_{var}.csv",
                                 "correction": "FETCH_SIZE x2 (gfx950; 16 B/lane per MI355X_MICROARCH.md, 4 B / 8 B "
-                                              "per lane by scripts/calib_4b.hip / calib_8b.hip)", "calibrated": True}
+                                              "per lane by the recorded calibration runs profiles/r01/calib_4b_*.csv "
+                                              "and profiles/r03/calib_8b_*.csv)", "calibrated": True}
     else:
         out[key] = None
         out[key + "_detail"] = {"fetch_size_raw_bytes": round(vals["FETCH_SIZE"]),

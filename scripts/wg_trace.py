@@ -1,6 +1,6 @@
 """Per-workgroup timeline of the last bit tile launch (diagnostics builds only:
 LIFE_WG_TRACE=1, loaded through LIFE_MI355X_LIB).  Runs the bench shape
-(65536^2, 20 generations from a 50 % soup) and summarises when workgroups
+(65536^2 or WG_TRACE_SHAPE=WxH, 20 generations from a 50 % soup) and summarises when workgroups
 started and ended, how many ran at once per CU and XCD, and how long each took.
     usage: LIFE_MI355X_LIB=build_exp/trace/liblife_mi355x.so python scripts/wg_trace.py [gens] [out.npy]
 """
@@ -16,7 +16,8 @@ import life_mi355x as lm  # noqa: E402
 
 gens = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 kernel = os.environ.get("WG_TRACE_KERNEL", "bit")  # byte: stamps after the load, the generations, the stores
-with lm.Life(65536, 65536, shards=1, kernel=kernel) as life:
+nx, ny = (int(v) for v in os.environ.get("WG_TRACE_SHAPE", "65536x65536").split("x"))
+with lm.Life(nx, ny, shards=1, kernel=kernel) as life:
     life.fill_random(1, 0.5)
     life.step(5)
     life.step(gens)

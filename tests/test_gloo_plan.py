@@ -103,7 +103,7 @@ def _worker(rank, world, port, nx, ny, dims, gens, seed, kernel, q):
 ])
 def test_plan_over_gloo(oracle, lm, kernel, world, nx, ny, gens):
     """Either encoding: 32-cell x /
-    K-row y aprons, up to K = 16 generations per exchange (temporal layouts),
+    K-row y aprons, up to K = 32 generations per exchange (temporal layouts),
     or the one-cell fallback when a block width is not a multiple of 32 or a
     partitioned block is shorter than K rows."""
     dims = lm.dims_create(world)

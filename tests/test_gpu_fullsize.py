@@ -186,3 +186,29 @@ def test_driver_shape_65536_band_vs_oracle(gpu, oracle):
             got = life.gather()[:, cols]
             band = oracle.life_run(band, gens, threads=_threads())
             np.testing.assert_array_equal(got, band[:, margin:margin + 2 * half], err_msg=f"after +{gens}")
+
+
+@pytest.mark.timeout(420)
+def test_c3_1000_generations_band_vs_oracle(gpu, oracle):
+    """configs[2] at its stated length: random 50 %
+    32768^2, seed 1, 1000 generations, bit AND byte kernels, pinned DIRECTLY to
+    the CPU oracle (3-life/life2d.c:104-130 restated) -- not only byte == bit,
+    which shares the bit-sliced rule.  The oracle steps a full-height band of
+    2048 + 2 x 1024 columns centred on the x = 0 seam (the periodic wrap and the
+    grid's banded last tile column), made by the same counter-based generator;
+    wrong values enter the band at its cut edges and move one cell per
+    generation, so after 1000 generations its inner 2048 columns are exact and
+    are compared cell by cell with both GPU grids (1.3e11 oracle cell-updates,
+    under a minute at 16 threads)."""
+    n, half, margin, gens = 32768, 1024, 1024, 1000
+    band = oracle.fill_random_window(n, n - half - margin, 0, 2 * (half + margin), n, seed=1, density=0.5)
+    cols = np.r_[n - half:n, 0:half]
+    got = {}
+    for kernel in ("bit", "byte"):
+        with gpu.Life(n, n, kernel=kernel) as life:
+            life.fill_random(1, 0.5)
+            life.step(gens)
+            got[kernel] = life.gather()[:, cols]
+    want = oracle.life_run(band, gens, threads=_threads())[:, margin:margin + 2 * half]
+    for kernel, g in got.items():
+        np.testing.assert_array_equal(g, want, err_msg=f"{kernel} after {gens} generations")

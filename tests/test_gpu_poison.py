@@ -10,8 +10,9 @@ not land fails here on EVERY run -- a zeroed buffer would pass whenever the
 expected grid is sparse (round 3's all-zero 17x3 result).
 
 The test functions are the parity tests themselves (one-generation, tiles,
-dataflow tiles, small grids, LOCAL shards, RCCL / LOCAL loopback, the
-reference's random grids), collected a second time in this module, where the
+dataflow tiles, small grids, LOCAL shards, the deep-halo schedules -- whose
+passes must never read an output buffer's stale apron rows beyond the
+extension -- RCCL / LOCAL loopback, the reference's random grids), collected a second time in this module, where the
 autouse fixture sets LIFE_POISON before each device is created.
 """
 import pytest
@@ -19,7 +20,8 @@ import pytest
 from test_gpu_golden import test_random_vs_reference_life_step  # noqa: F401
 from test_gpu_loopback import (test_loopback_initall_gather_and_frames,  # noqa: F401
                                test_loopback_no_overlap_and_toggle, test_loopback_parity)
-from test_gpu_parity import (test_gather_bits, test_multi_shard_local, test_single_shard,  # noqa: F401
+from test_gpu_parity import (test_deep_halo, test_deep_halo_exchange_count,  # noqa: F401
+                             test_gather_bits, test_multi_shard_local, test_single_shard,
                              test_small_grid_path, test_small_grid_windowed, test_temporal_multi_shard_local,
                              test_temporal_single_shard, test_wide_periodic_tile_columns)
 
