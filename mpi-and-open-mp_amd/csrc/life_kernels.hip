@@ -799,6 +799,8 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tflow_kernel(FArgs f)
     const int lane = threadIdx.x & 63;
     unsigned int *prev_flag = nullptr;  // thread 0: the finished item's tile counter
     unsigned int prev_val = 0;
+    int traced = 0;  // diagnostics builds: items 0..3 stamp pulled / dependencies met / stored
+    wg_trace(0);
     for (;;) {
         // ONE thread-0 region per iteration, behind the barrier that closes
         // the previous item: publish that item (its stores were drained by
@@ -820,6 +822,7 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tflow_kernel(FArgs f)
         // uniform: scalar registers, scalar arithmetic
         const uint32_t item = __builtin_amdgcn_readfirstlane(item_sh);
         if ((int64_t)item >= f.items) return;  // the whole workgroup leaves
+        if (LIFE_WG_TRACE && traced < 4) wg_trace(1 + 3 * traced);
         const uint32_t ntx = (uint32_t)f.ntx, nty = (uint32_t)f.nty;
         const uint32_t p = item / (uint32_t)tiles, k = item - p * (uint32_t)tiles;
         const uint32_t kr = k / ntx;
@@ -854,11 +857,13 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tflow_kernel(FArgs f)
             }
         }
         __syncthreads();
+        if (LIFE_WG_TRACE && traced < 4) wg_trace(2 + 3 * traced);
         const uint8_t *in = (p & 1) ? a.out : a.in;
         uint8_t *out = const_cast<uint8_t *>((p & 1) ? a.in : a.out);
         tile_body_bit<R, WRAPX, WRAPY, FLOW, NW>(a, in, out, tx, ty, xch);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
         __syncthreads();
+        if (LIFE_WG_TRACE && traced < 4) wg_trace(3 + 3 * traced++);
         prev_flag = f.done + ty * f.ntx + tx;
         prev_val = p + 1;
     }

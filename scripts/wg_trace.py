@@ -17,7 +17,8 @@ import life_mi355x as lm  # noqa: E402
 gens = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 kernel = os.environ.get("WG_TRACE_KERNEL", "bit")  # byte: stamps after the load, the generations, the stores
 nx, ny = (int(v) for v in os.environ.get("WG_TRACE_SHAPE", "65536x65536").split("x"))
-with lm.Life(nx, ny, shards=1, kernel=kernel) as life:
+flow = int(os.environ.get("WG_TRACE_FLOW", "0"))  # 1/2: the dataflow launch (one per call), items 0..3 stamped
+with lm.Life(nx, ny, shards=1, kernel=kernel, flow=flow) as life:
     life.fill_random(1, 0.5)
     life.step(5)
     life.step(gens)
@@ -30,6 +31,23 @@ with lm.Life(nx, ny, shards=1, kernel=kernel) as life:
     assert fn(buf, n) == 0
 t = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 16)
 t = t[t[:, 0] > 0]
+if flow:
+    # per workgroup: start, hw id, then (pulled, dependencies met, stored) of its first 4 items
+    t0 = int(t[:, 0].min())
+    st = np.where(t[:, 2:14] > 0, (t[:, 2:14].astype(np.int64) - t0) / 100.0, np.nan).reshape(-1, 4, 3)
+    wait = st[:, :, 1] - st[:, :, 0]
+    body = st[:, :, 2] - st[:, :, 1]
+    turn = st[:, 1:, 0] - st[:, :-1, 2]
+    q = lambda v: " ".join(f"{np.nanpercentile(v, p):.1f}" for p in (10, 50, 90, 99))  # noqa: E731
+    print(f"flow: {len(t)} workgroups; per item (pct 10/50/90/99, us)")
+    for i in range(4):
+        print(f"  item {i}: pulled at {q(st[:, i, 0])} | dep wait {q(wait[:, i])} | body {q(body[:, i])}")
+    print(f"  turnover (stored -> next pulled): {q(turn)}")
+    ends = st[:, :, 2].ravel()
+    ts = np.linspace(0, np.nanmax(ends), 31)
+    busy = [int(np.nansum((st[:, :, 1] <= x) & (st[:, :, 2] > x))) for x in ts]
+    print("items computing over time (first 4 per workgroup only):", busy)
+    sys.exit(0)
 t0 = int(t[:, 0].min())
 start = (t[:, 0].astype(np.int64) - t0) / 100.0  # us
 tiles = np.where(t[:, 2:] > 0, (t[:, 2:].astype(np.int64) - t0) / 100.0, np.nan)  # end of each tile
