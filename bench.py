@@ -327,15 +327,19 @@ def main():
         if n_gpus != 1:
             raise SystemExit("--loopback is a one-GPU mode")
         life.configure(lm.OPT_LOOPBACK, 1)
-    # The timed call times its launches only, each stamped by its own
-    # dispatch, so that no event packets sit between the ring, halo and
-    # interior work it measures (set_timing(2)); the overlapped schedule's
-    # phase events (the "phases" object of an N > 1 line) are recorded after
-    # the timed region and the parity check, over K more generations (one
-    # exchange at least: with the deep halo a short call may hold none).
-    # LIFE_BENCH_PHASES_TIMED=1 (or no warmup): the phase events inside the
-    # timed call.
+    # The timed call of a single-stream step (one shard, no partitioned
+    # axis: the N = 1 lines) carries one event pair around all its launches
+    # (set_timing(2) keeps it so).  A multi-stream step (N > 1, --loopback)
+    # is timed by its span only (set_timing(3)): per-launch events there put
+    # ~10 us between back-to-back launches (profiles/r05/c, d).  Its kernel
+    # statistics (the roofline object) and the overlapped schedule's phase
+    # events (the "phases" object) are then recorded after the timed region
+    # and the parity check, over K more generations (one exchange at least:
+    # with the deep halo a short call may hold none).
+    # LIFE_BENCH_PHASES_TIMED=1 (or no warmup): all of it inside the timed call.
     phases_timed = os.environ.get("LIFE_BENCH_PHASES_TIMED", "0") == "1" or a.warmup <= 0
+    multi = n_gpus > 1 or a.loopback
+    stats_after = multi and not phases_timed
     life.set_timing(True)
     life.step(a.warmup)
     life.sync()
@@ -352,7 +356,7 @@ def main():
         else:
             life.sync()
 
-    life.set_timing(True if phases_timed else 2)
+    life.set_timing(True if phases_timed else (3 if multi else 2))
     barrier_sync()
     t0 = time.perf_counter()
     life.step(a.steps)
@@ -372,8 +376,9 @@ def main():
     call = life.call_stats()  # host enqueue / device span of the timed call
     elapsed, host_enq, pass_enq, span = allmax([elapsed, call["host_enqueue_ms"], call["pass_enqueue_max_ms"],
                                                 call["device_span_ms"]])
-    avg_ms, launches, bytes_per_launch = life.kernel_stats()
-    updates_per_launch, valu_per_launch = life.kernel_work()
+    if not stats_after:
+        avg_ms, launches, bytes_per_launch = life.kernel_stats()
+        updates_per_launch, valu_per_launch = life.kernel_work()
     if phases_timed:
         ph = life.phase_stats()
     live = life.live_count()
@@ -388,12 +393,14 @@ def main():
     if n_gpus > 1 and not a.no_parity:
         parity = parity_vs_1gpu(a, life, grid, nx, ny, a.warmup + a.steps, elapsed, n_gpus, rank, dist,
                                 barrier_sync)
-    if not phases_timed and (n_gpus > 1 or a.loopback):
+    if stats_after:
         life.set_timing(True)
         life.step(lay.generations_per_exchange)
         life.sync()
         ph = life.phase_stats()
-    if n_gpus > 1 or a.loopback:
+        avg_ms, launches, bytes_per_launch = life.kernel_stats()
+        updates_per_launch, valu_per_launch = life.kernel_work()
+    if multi:
         exposed = allmax([ph["block_ms"] - ph["interior_ms"], ph["block_ms"], ph["halo_ms"]])
 
     if rank == 0:
@@ -436,6 +443,9 @@ def main():
             roofline = {"bound": "valu", "achieved": round(useful, 2), "peak": round(VALU_PEAK_TOPS, 2),
                         "unit": "Tlane-op/s", "frac": round(useful / VALU_PEAK_TOPS, 4), "traffic": traffic,
                         "kernel_avg_ms": round(avg_ms, 5), "kernel_launches": launches,
+                        "kernel_timing": ("HIP events on the launches of K generations after the timed call "
+                                          "(a multi-stream call is timed by its span only)") if stats_after
+                        else "HIP events on the timed call's stream",
                         "generations_per_launch": round(gens_per_launch, 3), "algorithmic_ops_per_launch": algo,
                         "issued": {"achieved": round(tops, 2), "frac": round(tops / VALU_PEAK_TOPS, 4),
                                    "ops_per_launch": valu_per_launch,

@@ -226,7 +226,10 @@ int life_dev_world(life_dev *d, int *world, int *dims0, int *dims1, int *nlocal,
  * records the overlapped schedule's phase events (life_dev_phase_stats: ring,
  * interior, halo, block); on = 2 times the launches only (their events are
  * stamped by the dispatches themselves), leaving no event packets between the
- * ring, halo and interior work of a partitioned step. */
+ * ring, halo and interior work of a partitioned step; on = 3 records only
+ * the call's span (life_dev_call_stats) on a multi-stream call -- per-launch
+ * events there put ~10 us between back-to-back launches (profiles/r05/c, d) --
+ * while a single-stream call keeps its one event pair around all launches. */
 int life_dev_set_timing(life_dev *d, int on);
 
 /* Execution-path switches (defaults 1): LIFE_OPT_SMALL_GRID lets a

@@ -186,6 +186,7 @@ struct life_dev {
     bool rank_mode = false;
     bool timing = false;
     bool phase_events = true;  // timing on: also the overlapped schedule's phase events (life_dev_set_timing 1)
+    bool launch_events = true;  // timing on: per-launch events of multi-stream calls (off: life_dev_set_timing 3)
     bool overlap = true;
     int block_gens = 0;  // tiles: generations per launch at most (LIFE_OPT_BLOCK_GENS; default_block_gens)
     int small_mode = 1;  // grids that fit one CU: 0 off, 1 VGPR kernel else LDS kernel, 2 LDS kernel,
@@ -518,7 +519,7 @@ int launch_timer(life_dev *d, Shard &s, int launches, TimedLaunch **t, bool *use
         *t = d->call_timer;
         return LIFE_OK;
     }
-    if (kEnvTimingMode == kTimeOff) return LIFE_OK;
+    if (kEnvTimingMode == kTimeOff || !d->launch_events) return LIFE_OK;
     int rc;
     *t = timer_slot(s, &rc);
     if (!*t) return rc;
@@ -540,7 +541,7 @@ int launch_region(life_dev *d, Shard &s, const life::Region &r, bool timed, hipS
         if (ev) HIPCHK(hipEventRecord(t->a, st));
     }
     HIPCHK(life::launch_step(s.lay, in, out, s.sink, r, wrap_of(d), st));
-    if (d->timing && timed) {
+    if (d->timing && timed && t) {  // (span-only timing books no launches)
         if (ev) HIPCHK(hipEventRecord(t->b, st));
         const bool bit = s.lay.kernel == LIFE_KERNEL_BIT;
         const int64_t cpu = bit ? 128 : 16;
@@ -625,7 +626,7 @@ int launch_tiles(life_dev *d, Shard &s, const life::TileRegion *r, int nreg, int
     HIPCHK(life::launch_tstep(s.lay, in, out, r, nreg, m, wrap_of(d), st, &valu, ext ? t->a : nullptr,
                               ext ? t->b : nullptr, xt));
     if (ev && !ext) HIPCHK(hipEventRecord(t->b, st));
-    if (d->timing && timed) {
+    if (d->timing && timed && t) {  // (span-only timing books no launches)
         const life::TileGeom g = life::tile_geom(life::extended_layout(s.lay, xt), m);
         for (int k = 0; k < nreg; k++) {
             // owned cells only (a deep-halo pass's apron rows are not counted)
@@ -646,22 +647,36 @@ int launch_tiles(life_dev *d, Shard &s, const life::TileRegion *r, int nreg, int
     return LIFE_OK;
 }
 
-// Block boundary of the overlapped schedule: both compute streams wait for
-// the interior (stream2), the ring (stream) and the halo (comm stream).
-int join_streams(Shard &s) {
-    HIPCHK(hipEventRecord(s.ev_int, s.stream2));
-    HIPCHK(hipStreamWaitEvent(s.stream, s.ev_int, 0));
-    HIPCHK(hipStreamWaitEvent(s.stream, s.ev_halo, 0));
-    HIPCHK(hipEventRecord(s.ev_join, s.stream));
-    HIPCHK(hipStreamWaitEvent(s.stream2, s.ev_join, 0));
-    return LIFE_OK;
+// The overlapped schedule of one exchange block (round 5, profiles/r05/c-d
+// kernel traces): the ring tiles, then the halo of their new state (pack,
+// RCCL / copies, unpack) on the compute stream `stream`, back to back in one
+// hardware queue; the interior tiles concurrently on `stream2`.  The block
+// ends with ONE cross-queue wait, placed on the stream whose work is
+// predicted to end first: a queue that reaches a wait whose event has
+// already fired passes it at once, while one that must sleep on it woke
+// ~20 us after the event on MI355X (the halo's end to the next pass, r05d).
+// So the work carries on in the queue predicted to finish last: the halo's
+// (`stream`, which then waits for the interior) when the block is under
+// three rounds of tiles -- small shards, where ring + halo outlast the
+// interior (RCCL loopback, r05e: 16384x32768 1.1 rounds, 32768^2 2.2 rounds
+// +8 % on the halo side; 32768x65536 4.3 rounds +1.7 % on the interior's) --
+// else the interior's (`stream2` waits for the halo and the two handles are
+// swapped, so `stream` always names the one that carries on).
+// LIFE_JOIN (read once): 0 auto, 1 always the halo's stream, 2 always the
+// interior's.
+int join_mode() {
+    static const int v = [] {
+        const char *e = getenv("LIFE_JOIN");
+        const int m = e ? atoi(e) : 0;
+        return m >= 0 && m <= 2 ? m : 0;
+    }();
+    return v;
 }
 
 // Phase timing of one overlapped block (timing on): ring0 before the ring
-// kernels on the compute stream, ring1 after them; the comm stream waits for
-// the ring (ev_ring) and records halo0, then the exchange, halo1; the
-// interior kernel is bracketed on the second compute stream; `end` after the
-// join on the compute stream.  Without timing: just the ring -> comm order.
+// kernels on the compute stream, ring1 after them, halo0 / halo1 around the
+// halo on the same stream; the interior kernel is bracketed on the second
+// compute stream; `end` after the join on the stream that carries on.
 int phase_begin(life_dev *d, Shard &s, PhaseEvents **pe) {
     *pe = nullptr;
     if (!d->timing || !d->phase_events) return LIFE_OK;
@@ -672,24 +687,36 @@ int phase_begin(life_dev *d, Shard &s, PhaseEvents **pe) {
     return LIFE_OK;
 }
 int phase_ring(Shard &s, PhaseEvents *pe) {
-    if (pe) HIPCHK(hipEventRecord(pe->ring1, s.stream));
-    HIPCHK(hipEventRecord(s.ev_ring, s.stream));
-    HIPCHK(hipStreamWaitEvent(s.comm_stream, s.ev_ring, 0));
-    if (pe) HIPCHK(hipEventRecord(pe->halo0, s.comm_stream));
+    if (pe) {
+        HIPCHK(hipEventRecord(pe->ring1, s.stream));
+        HIPCHK(hipEventRecord(pe->halo0, s.stream));
+    }
     return LIFE_OK;
 }
-int phase_end(life_dev *d, const std::vector<PhaseEvents *> &pe) {
+// halo_side[si]: shard si carries on in its halo's stream (see join_mode).
+int phase_end(life_dev *d, const std::vector<PhaseEvents *> &pe, const std::vector<char> &halo_side) {
     for (size_t si = 0; si < d->shards.size(); ++si) {
         Shard &s = d->shards[si];
         HIPCHK(hipSetDevice(s.device));
-        // halo1 before ev_halo: `end` (after the join on ev_halo) then
-        // implies halo1 has completed too
-        if (pe[si]) HIPCHK(hipEventRecord(pe[si]->halo1, s.comm_stream));
-        HIPCHK(hipEventRecord(s.ev_halo, s.comm_stream));
-        CHK(join_streams(s));
+        if (pe[si]) HIPCHK(hipEventRecord(pe[si]->halo1, s.stream));
+        if (halo_side[si] || stream_priorities()) {
+            HIPCHK(hipEventRecord(s.ev_int, s.stream2));
+            HIPCHK(hipStreamWaitEvent(s.stream, s.ev_int, 0));
+        } else {
+            HIPCHK(hipEventRecord(s.ev_halo, s.stream));
+            HIPCHK(hipStreamWaitEvent(s.stream2, s.ev_halo, 0));
+            std::swap(s.stream, s.stream2);
+        }
         if (pe[si]) HIPCHK(hipEventRecord(pe[si]->end, s.stream));
     }
     return LIFE_OK;
+}
+// The auto rule of join_mode: ring + interior tiles under three rounds of
+// resident workgroups.
+bool carry_on_halo_side(int64_t block_items, int slots) {
+    const int m = join_mode();
+    if (m != 0) return m == 1;
+    return slots > 0 && block_items < 3 * (int64_t)slots;
 }
 
 // Generations the next temporal launch runs (remaining > 0): a step call
@@ -752,6 +779,7 @@ int generation_block(life_dev *d, int m, bool last) {
         return LIFE_OK;
     }
     std::vector<PhaseEvents *> pe(d->shards.size(), nullptr);
+    std::vector<char> halo_side(d->shards.size(), 0);
     for (size_t si = 0; si < d->shards.size(); ++si) {
         Shard &s = d->shards[si];
         HIPCHK(hipSetDevice(s.device));
@@ -799,6 +827,9 @@ int generation_block(life_dev *d, int m, bool last) {
         CHK(launch(ring, n, false, s.stream));
         CHK(phase_ring(s, pe[si]));
         const life::TileRegion inner{ca, cb, ra, rb};
+        int64_t items = life::region_items(g, inner);
+        for (int k = 0; k < n; k++) items += life::region_items(g, ring[k]);
+        halo_side[si] = carry_on_halo_side(items, life::tile_slots(s.lay)) ? 1 : 0;
         if (pe[si]) HIPCHK(hipEventRecord(pe[si]->int0, s.stream2));
         if (rb > ra && cb > ca) CHK(launch(&inner, 1, true, s.stream2));
         if (pe[si]) HIPCHK(hipEventRecord(pe[si]->int1, s.stream2));
@@ -811,8 +842,8 @@ int generation_block(life_dev *d, int m, bool last) {
         for (Shard &s : d->shards) s.cur ^= 1;
         return exchange(d, 0, false);
     }
-    CHK(exchange(d, 1, true));
-    CHK(phase_end(d, pe));
+    CHK(exchange(d, 1, false));  // halo of nxt, behind the ring on the compute streams
+    CHK(phase_end(d, pe, halo_side));
     for (Shard &s : d->shards) s.cur ^= 1;
     return LIFE_OK;
 }
@@ -852,8 +883,10 @@ int generation(life_dev *d) {
         if (rb > ra && ub > ua) CHK(launch_region(d, s, life::Region{ua, ub, ra, rb}, true, s.stream2));
         if (pe[si]) HIPCHK(hipEventRecord(pe[si]->int1, s.stream2));
     }
-    CHK(exchange(d, 1, true));  // halo of nxt on the comm streams
-    CHK(phase_end(d, pe));
+    CHK(exchange(d, 1, false));  // halo of nxt, behind the ring on the compute streams
+    // one-generation launches are short: carry on in the interior's stream
+    // unless LIFE_JOIN says otherwise
+    CHK(phase_end(d, pe, std::vector<char>(d->shards.size(), join_mode() == 1 ? 1 : 0)));
     for (Shard &s : d->shards) s.cur ^= 1;
     return LIFE_OK;
 }
@@ -1698,7 +1731,8 @@ int life_dev_set_timing(life_dev *d, int on) {
     d->ph_ring = d->ph_int = d->ph_halo = d->ph_block = 0.0;
     d->ph_blocks = 0;
     d->timing = on != 0;
-    d->phase_events = on != 2;
+    d->phase_events = on == 1;
+    d->launch_events = on != 3;
     d->acc_ms = 0.0;
     d->acc_launches = 0;
     d->acc_bytes = 0.0;

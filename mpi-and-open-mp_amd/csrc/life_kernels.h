@@ -85,6 +85,7 @@ constexpr int64_t kTemporalSlackRows = 8 * 96;
 // in `out` when passes is odd, else in `in`.
 bool flow_ok(const life_layout &L, int m);
 int flow_slots(const life_layout &L);  // resident workgroups of L's dataflow kernel on this device
+int tile_slots(const life_layout &L);  // resident workgroups of L's per-launch tile kernel on this device
 // ev0 / ev1 (optional): events stamped with the kernel dispatch's own start
 // and end (hipExtLaunchKernel) -- no event packets between launches.
 hipError_t launch_tflow(const life_layout &L, const uint8_t *in, uint8_t *out, int m, int64_t passes,

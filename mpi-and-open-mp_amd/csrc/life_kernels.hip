@@ -353,6 +353,12 @@ struct XchB {
 // read beyond the tile, absorbed by the ghost lanes.  Only the loads and
 // stores differ (per-lane rows); the generation loop is the tile's.  gsh = 6:
 // an ordinary tile (nb = 1).
+// LIFE_FLOW_EXP (timing-only diagnostics builds, results may be stale; never
+// in the product build): bit 1 plain window loads in the dataflow tiles, 2
+// plain stores, 4 no store drain before the hand-off flag.
+#ifndef LIFE_FLOW_EXP
+#define LIFE_FLOW_EXP 0
+#endif
 // LIFE_FAST_WRAP: a tile's wrapped pair column and first row by one
 // conditional add / subtract instead of a 64-bit remainder (per lane for the
 // column) when the axis is long enough for the index to be at most one
@@ -416,7 +422,7 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             uint64_t q;
-            if (FLOW)
+            if (FLOW && !(LIFE_FLOW_EXP & 1))
                 q = __hip_atomic_load(reinterpret_cast<uint64_t *>(const_cast<uint8_t *>(p) + voff),
                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             else
@@ -528,7 +534,7 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
         if (r < r0 || r >= r1) continue;
         if (st && yb + r < ylim) {
             const uint64_t v = (uint64_t)ve[r] | ((uint64_t)vo[r] << 32);
-            if (FLOW == 1)
+            if (FLOW == 1 && !(LIFE_FLOW_EXP & 2))
                 __hip_atomic_store(reinterpret_cast<uint64_t *>(q), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             else
                 *reinterpret_cast<uint64_t *>(q) = v;
@@ -861,7 +867,7 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tflow_kernel(FArgs f)
         const uint8_t *in = (p & 1) ? a.out : a.in;
         uint8_t *out = const_cast<uint8_t *>((p & 1) ? a.in : a.out);
         tile_body_bit<R, WRAPX, WRAPY, FLOW, NW>(a, in, out, tx, ty, xch);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
+        if (!(LIFE_FLOW_EXP & 4)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
         __syncthreads();
         if (LIFE_WG_TRACE && traced < 4) wg_trace(3 + 3 * traced++);
         prev_flag = f.done + ty * f.ntx + tx;
@@ -1778,6 +1784,17 @@ static int tstep_bit_slots() {
     const int k = temporal_rows(true) * 64 + tile_waves(true);
     if (k != key) {
         cached = slots_of(tstep_bit_fn(), 64 * tile_waves(true));
+        key = k;
+    }
+    return cached;
+}
+
+int tile_slots(const life_layout &L) {
+    if (is_bit(L)) return tstep_bit_slots();
+    static int cached = 0, key = -1;
+    const int k = temporal_rows(false);
+    if (k != key) {
+        cached = slots_of(byte_k<32>(Wrap{true, true}), 64 * kStackWaves);
         key = k;
     }
     return cached;

@@ -70,9 +70,11 @@ def test_loopback_no_overlap_and_toggle(gpu, oracle, kernel):
 @pytest.mark.parametrize("rccl", [None, "rank"], ids=["local", "rccl"])
 def test_loopback_timing_modes(gpu, oracle, rccl):
     """set_timing(True) records the overlapped schedule's phase events,
-    set_timing(2) (bench.py's timed call) times the launches only: no phase
-    blocks, the tile launches still counted and timed, the same cells."""
-    nx, ny, gens = 16384, 1024, 64  # 4 x 3 interior tiles: the interior is its own launch
+    set_timing(2) times the launches only: no phase blocks, the tile launches
+    still counted and timed; set_timing(3) (bench.py's timed call of a
+    multi-stream step) records the call's span only: no launches booked, a
+    device span; the same cells throughout."""
+    nx, ny, gens = 16384, 1024, 96  # 4 x 3 interior tiles: the interior is its own launch
     g0 = oracle.fill_random(nx, ny, seed=17, density=0.5)
     with _make(gpu, nx, ny, "bit", rccl) as life:
         life.upload(g0)
@@ -86,11 +88,17 @@ def test_loopback_timing_modes(gpu, oracle, rccl):
         ms1, n1, _ = life.kernel_stats()
         assert n1 == 2 and ms1 > 0  # the interior launches
         life.set_timing(2)
-        life.step(gens - 24)
+        life.step(40)
         ph = life.phase_stats()
         assert ph["blocks"] == 0 and ph["block_ms"] == 0.0
         ms2, n2, _ = life.kernel_stats()
         assert n2 == 4 and ms2 > 0  # 10 x 4 generations
+        np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, 64, threads=4))
+        life.set_timing(3)
+        life.step(gens - 64)
+        assert life.phase_stats()["blocks"] == 0
+        assert life.kernel_stats()[1] == 0
+        assert life.call_stats()["device_span_ms"] > 0
         np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, gens, threads=4))
 
 
