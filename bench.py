@@ -93,9 +93,10 @@ def parse():
     p.add_argument("--no-parity", action="store_true")
     p.add_argument("--rank-mode", action="store_true",
                    help="one-process-per-GPU set-up (gloo bootstrap, RCCL communicator) even at world 1")
-    p.add_argument("--flow", type=int, default=None, choices=[0, 1, 2],
+    p.add_argument("--flow", type=int, default=None, choices=[0, 1, 2, 3],
                    help="LIFE_OPT_FLOW: single-shard bit tiles as one persistent dataflow launch per step call "
-                        "(1 write-through, 2 fenced hand-off; 0 per-launch tiles; default: the library's)")
+                        "(1 write-through, 2 fenced hand-off; 0 per-launch tiles; 3 automatic by rounds per pass; "
+                        "default: the library's, 3)")
     p.add_argument("--no-overlap", action="store_true",
                    help="partitioned shards: every tile in one launch, then the halo exchange (LIFE_OPT_OVERLAP 0) "
                         "instead of ring / interior / halo on three streams")

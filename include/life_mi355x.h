@@ -82,11 +82,13 @@ int life_dims_choose(int64_t nx, int64_t ny, int n, int policy, int dims[2]);
 #define LIFE_HALO_FILL 2   /* axis not partitioned (dims[d] == 1): wrapped inside the shard */
 #define LIFE_HALO_COLUMN 0 /* cells x in [index, index+width) of padded rows [first, first+count) */
 #define LIFE_HALO_ROW 1    /* padded rows [index, index+width), cells x in [first, first+count) */
+#define LIFE_HALO_CORNER 2 /* as a column op: cells x in [index, index+width) of padded rows [first, first+count) */
 typedef struct {
-    int32_t phase; /* 0: x (columns) first, then 1: y (rows incl. corners) */
+    int32_t phase; /* 0: x (columns) first, then 1: y (rows incl. corners); both axes
+                      exchanged with temporal aprons: all in phase 0, corners explicit */
     int32_t kind;  /* LIFE_HALO_SEND / RECV / FILL */
     int32_t peer;  /* global shard rank, -1 for FILL */
-    int32_t what;  /* LIFE_HALO_COLUMN / LIFE_HALO_ROW */
+    int32_t what;  /* LIFE_HALO_COLUMN / LIFE_HALO_ROW / LIFE_HALO_CORNER */
     int64_t index; /* first column x, or first padded row */
     int64_t first; /* first padded row (column op) or first cell x (row op) */
     int64_t count; /* rows (column op) or cells (row op) */
@@ -271,16 +273,18 @@ int life_dev_set_timing(life_dev *d, int on);
  * are identical either way.  The grid must be at least one halo deep
  * (generations_per_exchange rows). */
 #define LIFE_OPT_LOOPBACK 6
-/* LIFE_OPT_FLOW (default 0 since the pair tiles -- per-launch tiles measured
- * 3-5 % faster, DESIGN.md §5 -- or LIFE_FLOW from the environment): a step call
+/* LIFE_OPT_FLOW (default 3, automatic, or LIFE_FLOW from the environment): a step call
  * on a single shard whose axes both wrap inside it (bit encoding, width a
  * multiple of 64) runs its whole passes of m generations (m = the block
  * size, LIFE_OPT_BLOCK_GENS; at least 4 passes) as ONE persistent launch: workgroups pull
  * (pass, tile) items in order and a tile starts when the tiles its window
  * reads have finished the previous pass, so no pass boundary drains the chip;
  * the remainder runs as an ordinary launch.  1: write-through hand-off
- * stores; 2: plain stores + a release fence per tile; 0: off.  The byte
- * encoding always runs per-launch tiles.  Same results. */
+ * stores; 2: plain stores + a release fence per tile; 0: off; 3: form 1
+ * when a pass is under 5 rounds of resident workgroups (its launch tail
+ * would idle the chip: 32768^2), else off (65536^2, where the per-launch
+ * tiles measured 3 % faster).  The byte encoding always runs
+ * per-launch tiles.  Same results. */
 #define LIFE_OPT_FLOW 7
 /* LIFE_OPT_FLOW_CHUNK (default 0 = automatic): the dataflow launch's queue
  * head is a 32-bit counter, so a step call's passes are split over several

@@ -102,6 +102,7 @@ struct Shard {
     size_t flow_words = 0;
     bool flow_used = false;  // a dataflow launch since the last sync checked its error word
     std::vector<life_halo_op> plan;
+    bool corners = false;  // the plan exchanges the four corner blocks itself (fused, one phase)
     std::vector<TimedLaunch> timers;
     size_t timers_used = 0;
     std::vector<PhaseEvents> phases;
@@ -123,7 +124,10 @@ static const int kEnvBlockGens = [] {
     const int v = e ? atoi(e) : 0;
     return v >= 1 && v <= 32 ? v : 0;
 }();
-// LIFE_FLOW (0/1/2) sets LIFE_OPT_FLOW's default at load time; default 0.
+// LIFE_FLOW (0/1/2/3) sets LIFE_OPT_FLOW's default at load time; default 3,
+// automatic (round 5): the dataflow form where a pass is only a few rounds
+// of resident workgroups, so that a launch per pass would idle the chip in
+// its tail (flow_auto below), the per-launch tiles elsewhere.
 // With the natural-word tiles (384-row windows, 20 generations per pass) the
 // dataflow form won (65536^2 95 -> 100 T, profiles/r02/flow_ab.txt); the
 // pair tiles are half as tall, their items half as long, and the per-item
@@ -133,8 +137,15 @@ static const int kEnvBlockGens = [] {
 // (profiles/r03/r4g).
 static const int kEnvFlow = [] {
     const char *e = getenv("LIFE_FLOW");
-    const int v = e ? atoi(e) : 0;
-    return v >= 0 && v <= 2 ? v : 0;
+    const int v = e ? atoi(e) : 3;
+    return v >= 0 && v <= 3 ? v : 3;
+}();
+// LIFE_FLOW_AUTO_ROUNDS (measurement knob, default 5): LIFE_OPT_FLOW 3 takes
+// the dataflow form when a pass holds fewer rounds of resident workgroups.
+static const double kFlowAutoRounds = [] {
+    const char *e = getenv("LIFE_FLOW_AUTO_ROUNDS");
+    const double v = e ? atof(e) : 0.0;
+    return v > 0.0 ? v : 5.0;
 }();
 // LIFE_DEEP_HALO (0/1, default 1) sets LIFE_OPT_DEEP_HALO's default at load
 // time (generation_block).
@@ -291,7 +302,7 @@ int shard_alloc(life_dev *d, Shard &s) {
     HIPCHK(hipEventCreateWithFlags(&s.ev_halo, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&s.ev_sync, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&s.ev_entry, hipEventDisableTiming));
-    const size_t col_bytes = (size_t)(2 * s.lay.h * life::column_bytes_per_row(s.lay));
+    const size_t col_bytes = (size_t)life::column_stage_bytes(s.lay);
     HIPCHK(hipMalloc(&s.col_send, col_bytes));
     HIPCHK(hipMalloc(&s.col_recv, col_bytes));
     HIPCHK(hipMalloc(&s.d_count, 2 * sizeof(unsigned long long)));
@@ -309,6 +320,7 @@ int shard_alloc(life_dev *d, Shard &s) {
         return LIFE_EINVAL;
     }
     s.plan.assign(ops, ops + n);
+    s.corners = std::any_of(s.plan.begin(), s.plan.end(), [](const life_halo_op &o) { return o.what == LIFE_HALO_CORNER; });
     return LIFE_OK;
 }
 
@@ -374,19 +386,33 @@ int local_order(life_dev *d, bool comm, int phase, int kind) {
 }
 
 // Pointer + size of the message of op `o` (the slot-th send or recv of its
-// phase): column ops go through the staging slots, row ops are whole padded
-// rows sent straight from / received straight into the buffer (every shard
-// of one Cartesian column has the same pitch).
+// kind among its phase's ops of the same `what`): column ops go through the
+// staging slots, corner ops (the fused plan) through the corner slots behind
+// them, row ops are whole padded rows sent straight from / received straight
+// into the buffer (every shard of one Cartesian column has the same pitch).
 void op_buffer(const Shard &s, const life_halo_op &o, int slot, uint8_t *base, uint8_t **ptr, size_t *bytes) {
+    const size_t cbr = (size_t)life::column_bytes_per_row(s.lay);
+    uint8_t *st = o.kind == LIFE_HALO_SEND ? s.col_send : s.col_recv;
     if (o.what == LIFE_HALO_COLUMN) {
-        const size_t per = (size_t)(s.lay.h * life::column_bytes_per_row(s.lay));
-        uint8_t *st = o.kind == LIFE_HALO_SEND ? s.col_send : s.col_recv;
+        const size_t per = (size_t)s.lay.h * cbr;
         *ptr = st + (size_t)slot * per;
+        *bytes = per;
+    } else if (o.what == LIFE_HALO_CORNER) {
+        const size_t per = (size_t)s.lay.yapron * cbr;
+        *ptr = st + 2 * (size_t)s.lay.h * cbr + (size_t)slot * per;
         *bytes = per;
     } else {
         *ptr = base + o.index * s.lay.pitch;
         *bytes = (size_t)(o.width * s.lay.pitch);
     }
+}
+
+// Staging slot of plan op i: earlier ops of its phase with the same kind and what.
+int op_slot(const std::vector<life_halo_op> &plan, size_t i) {
+    int n = 0;
+    for (size_t k = 0; k < i; k++)
+        n += plan[k].phase == plan[i].phase && plan[k].kind == plan[i].kind && plan[k].what == plan[i].what;
+    return n;
 }
 
 // One halo phase on buffer `which` of every local shard, on stream sel.
@@ -405,21 +431,23 @@ int run_phase(life_dev *d, int phase, int which_rel, bool on_comm) {
             }
         return LIFE_OK;
     }
+    bool any = false;  // a fused plan (both axes in phase 0) leaves phase 1 empty
+    for (const life_halo_op &o : d->shards[0].plan) any |= o.phase == phase;
+    if (!any) return LIFE_OK;
     if (phase == 0)
         for (Shard &s : d->shards) {
             HIPCHK(hipSetDevice(s.device));
-            HIPCHK(life::launch_pack_columns(s.lay, buf_of(s), s.col_send, stream_of(s)));
+            HIPCHK(life::launch_pack_columns(s.lay, buf_of(s), s.col_send, stream_of(s), s.corners));
         }
     if (d->transport == LIFE_XPORT_RCCL) {
         NCCLCHK(ncclGroupStart());
         for (Shard &s : d->shards) {
-            int ns = 0, nr = 0;
-            for (const life_halo_op &o : s.plan) {
+            for (size_t i = 0; i < s.plan.size(); i++) {
+                const life_halo_op &o = s.plan[i];
                 if (o.phase != phase) continue;
                 uint8_t *p;
                 size_t nb;
-                const int slot = o.kind == LIFE_HALO_SEND ? ns++ : nr++;
-                op_buffer(s, o, slot, buf_of(s), &p, &nb);
+                op_buffer(s, o, op_slot(s.plan, i), buf_of(s), &p, &nb);
                 if (o.kind == LIFE_HALO_SEND)
                     NCCLCHK(ncclSend(p, nb, ncclUint8, o.peer, s.comm, stream_of(s)));
                 else
@@ -431,11 +459,11 @@ int run_phase(life_dev *d, int phase, int which_rel, bool on_comm) {
         CHK(local_order(d, on_comm, phase, LIFE_HALO_RECV));
         for (Shard &s : d->shards) {
             HIPCHK(hipSetDevice(s.device));
-            int nr = 0;
             std::vector<int> seen_from;  // recvs from each peer so far
-            for (const life_halo_op &o : s.plan) {
+            for (size_t i = 0; i < s.plan.size(); i++) {
+                const life_halo_op &o = s.plan[i];
                 if (o.phase != phase || o.kind != LIFE_HALO_RECV) continue;
-                const int slot = nr++;
+                const int slot = op_slot(s.plan, i);
                 int kth = 0;  // this is the kth recv from o.peer
                 for (int p : seen_from) kth += p == o.peer;
                 seen_from.push_back(o.peer);
@@ -445,15 +473,15 @@ int run_phase(life_dev *d, int phase, int which_rel, bool on_comm) {
                     return LIFE_ESTATE;
                 }
                 // matching send: the kth send from src to s.rank
-                int ns = 0, cnt = 0;
+                int cnt = 0;
                 const life_halo_op *match = nullptr;
                 int match_slot = -1;
-                for (const life_halo_op &q : src->plan) {
+                for (size_t k = 0; k < src->plan.size(); k++) {
+                    const life_halo_op &q = src->plan[k];
                     if (q.phase != phase || q.kind != LIFE_HALO_SEND) continue;
-                    const int qs = ns++;
                     if (q.peer == s.rank && cnt++ == kth) {
                         match = &q;
-                        match_slot = qs;
+                        match_slot = op_slot(src->plan, k);
                         break;
                     }
                 }
@@ -480,7 +508,7 @@ int run_phase(life_dev *d, int phase, int which_rel, bool on_comm) {
     if (phase == 0)
         for (Shard &s : d->shards) {
             HIPCHK(hipSetDevice(s.device));
-            HIPCHK(life::launch_unpack_columns(s.lay, buf_of(s), s.col_recv, stream_of(s)));
+            HIPCHK(life::launch_unpack_columns(s.lay, buf_of(s), s.col_recv, stream_of(s), s.corners));
         }
     return LIFE_OK;
 }
@@ -1197,6 +1225,14 @@ static int step_flow(life_dev *d, int64_t generations, int64_t *done) {
     // the per-launch tiles (profiles/r03/r4d); the dataflow form pays from
     // about 4 passes (0.474 ms per 12-generation pass in long runs)
     if (passes < kFlowMinPasses || !life::flow_ok(L, m)) return LIFE_OK;
+    // automatic: the dataflow form (write-through hand-off) when a pass is
+    // under kFlowAutoRounds rounds of resident workgroups -- 32768^2 (2.2
+    // rounds of 768) +8 %, 32768 x 65536 (4.3) +1 %, 65536^2 (8.6) -3 %
+    // (profiles/r05/a)
+    int form = d->flow;
+    if (form == 3)
+        form = (double)life::flow_items_per_pass(L, m) < kFlowAutoRounds * (double)life::flow_slots(L) ? 1 : 0;
+    if (form == 0) return LIFE_OK;
     const life::TileGeom g = life::tile_geom(L, m);
     const size_t words = (size_t)(2 + g.ntx * g.nty);
     if (words > s.flow_words) {
@@ -1215,7 +1251,7 @@ static int step_flow(life_dev *d, int64_t generations, int64_t *done) {
     // past the last item: split the passes so that items + grid stays below
     // 2^31 per launch (life::flow_chunk_passes), flipping the buffer parity
     // per chunk.
-    const int64_t tiles = g.ntx * g.nty;
+    const int64_t tiles = life::flow_items_per_pass(L, m);
     const int64_t per = life::flow_chunk_passes(tiles, life::flow_slots(L), d->flow_chunk);
     if (per < 1) return LIFE_OK;  // a grid too large for one pass per launch: per-launch tiles
     for (int64_t left = passes; left > 0;) {
@@ -1226,7 +1262,7 @@ static int step_flow(life_dev *d, int64_t generations, int64_t *done) {
         const bool ext = ev && kEnvTimingMode == kTimeExt;
         if (ev && !ext) HIPCHK(hipEventRecord(t->a, s.stream));
         HIPCHK(life::launch_tflow(L, s.buf[s.cur], s.buf[s.cur ^ 1], m, n, s.flow, s.flow + 2, wrap_of(d),
-                                  d->flow, s.stream, ext ? t->a : nullptr, ext ? t->b : nullptr));
+                                  form, s.stream, ext ? t->a : nullptr, ext ? t->b : nullptr));
         if (ev && !ext) HIPCHK(hipEventRecord(t->b, s.stream));
         if (d->timing) {
             const double cells = (double)L.w * (double)L.h;
@@ -1668,7 +1704,7 @@ int life_dev_configure(life_dev *d, int option, int value) {
         d->block_gens = value > 0 ? value : default_block_gens(d->kernel);
         return LIFE_OK;
     case LIFE_OPT_FLOW:
-        if (value < 0 || value > 2) return LIFE_EINVAL;
+        if (value < 0 || value > 3) return LIFE_EINVAL;
         d->flow = value;
         return LIFE_OK;
     case LIFE_OPT_DEEP_HALO:
@@ -1708,6 +1744,8 @@ int life_dev_configure(life_dev *d, int option, int value) {
         const int n = life::halo_plan(d->nx, d->ny, d->dims[0], d->dims[1], s.rank, d->kernel, d->loop, ops, 16);
         if (n < 0) return LIFE_EINVAL;
         s.plan.assign(ops, ops + n);
+        s.corners =
+            std::any_of(s.plan.begin(), s.plan.end(), [](const life_halo_op &o) { return o.what == LIFE_HALO_CORNER; });
         CHK(exchange(d, 0, false));
         return life_dev_sync(d);
     }

@@ -84,6 +84,8 @@ constexpr int64_t kTemporalSlackRows = 8 * 96;
 // Pass p reads `in` for even p and `out` for odd p: after it, the result is
 // in `out` when passes is odd, else in `in`.
 bool flow_ok(const life_layout &L, int m);
+// work items of one dataflow pass (tiles, or tiles + banded items of a banded last column)
+int64_t flow_items_per_pass(const life_layout &L, int m);
 int flow_slots(const life_layout &L);  // resident workgroups of L's dataflow kernel on this device
 int tile_slots(const life_layout &L);  // resident workgroups of L's per-launch tile kernel on this device
 // ev0 / ev1 (optional): events stamped with the kernel dispatch's own start
@@ -155,10 +157,19 @@ inline int64_t column_bytes_per_row(const life_layout &L) {
     if (L.xapron == 1) return 1;
     return L.kernel == LIFE_KERNEL_BIT ? 8 : 32;
 }
+// corners (the fused one-phase plan, life_halo_plan): also the four K x
+// xapron corner blocks behind the two columns, K = yapron rows each.  Send
+// slots 2h + cK + r, c in the plan's direction order SE, SW, NE, NW: my
+// bottom-right, bottom-left, top-right, top-left K rows; receive slots in the
+// same order: my top-left, top-right, bottom-left, bottom-right apron corner.
 hipError_t launch_pack_columns(const life_layout &L, const uint8_t *buf, uint8_t *stage,
-                               hipStream_t s);
+                               hipStream_t s, bool corners = false);
 hipError_t launch_unpack_columns(const life_layout &L, uint8_t *buf, const uint8_t *stage,
-                                 hipStream_t s);
+                                 hipStream_t s, bool corners = false);
+// staging bytes of one direction (send or receive) of a shard's exchange
+inline int64_t column_stage_bytes(const life_layout &L) {
+    return (2 * L.h + (L.xapron > 1 ? 4 * L.yapron : 0)) * column_bytes_per_row(L);
+}
 // Temporal layouts: a periodic x axis inside one shard is wrapped by the
 // stencil (whole lane columns) when w is a multiple of the x-apron (64 bit
 // cells, 32 byte cells); otherwise the shard fills its own aprons from its own

@@ -787,24 +787,32 @@ __global__ __launch_bounds__(64 * NW, LIFE_BYTE_WPE) void tstep_byte_kernel(TArg
 // polling wave's lanes read the flags `sc1`, a barrier, then every wave loads.
 struct FArgs {
     TArgs t;                         // geometry, m; t.in / t.out: buffers of pass 0
-    int64_t ntx, nty, items;         // items = passes * ntx * nty
+    int64_t ntx, nty, items;         // items = passes * per_pass
+    // BAND: the last tile column (t.bcol) as banded items of B = 64 >> t.gsh
+    // tile rows; a pass is ngroups groups of B tile rows, each (ntx - 1) * B
+    // ordinary items then one banded item (tile rows past nty: no-op items)
+    int64_t per_pass, ngroups, B;
     unsigned int *head;              // queue head (zeroed before the launch), then an error word: 1 + the
                                      // last item whose dependency wait timed out (0: none)
     unsigned int *done;              // per tile: passes completed (zeroed before the launch)
 };
 
-// No banded column here: the banded items in this loop cost the ordinary
-// tiles 2.5 % (code size in the persistent loop; profiles/r02/r2x: b0 / b1 vs
-// base), more than they save.
-template <int R, bool WRAPX, bool WRAPY, int FLOW, int NW>
+// BAND (a last tile column owning o <= 30 pairs: 32768^2's 16, 16384^2's
+// 8): that column runs as banded items, as tstep_bit_kernel does, instead of
+// full-width tiles that waste (64 - o - 2) / 64 of their lanes.  Without it
+// the instance has no banded code in its loop (the banded items cost the
+// ordinary tiles 2.5 % there, code size in the persistent loop;
+// profiles/r02/r2x).
+template <int R, bool WRAPX, bool WRAPY, int FLOW, int NW, bool BAND = false>
 __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tflow_kernel(FArgs f) {
     __shared__ XchB<NW> xch;
     __shared__ unsigned int item_sh;
     const TArgs &a = f.t;
     const int64_t tiles = f.ntx * f.nty;
     const int lane = threadIdx.x & 63;
-    unsigned int *prev_flag = nullptr;  // thread 0: the finished item's tile counter
+    unsigned int *prev_flag = nullptr;  // wave 0, lanes < prev_n: the finished item's tile counters
     unsigned int prev_val = 0;
+    int prev_n = 0;
     int traced = 0;  // diagnostics builds: items 0..3 stamp pulled / dependencies met / stored
     wg_trace(0);
     for (;;) {
@@ -814,7 +822,7 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tflow_kernel(FArgs f)
         // regions on either side of the loop's back edge were merged by the
         // compiler into a region that lanes 1..63 of wave 0 never wait for:
         // the workgroup then re-ran its item forever.)
-        if (threadIdx.x == 0) {
+        if (!BAND && threadIdx.x == 0) {
             if (prev_flag) {
                 if (FLOW == 2) {
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -824,20 +832,58 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tflow_kernel(FArgs f)
             }
             item_sh = atomicAdd(f.head, 1u);
         }
+        if (BAND && threadIdx.x < 64) {  // one wave-0 region: a banded item publishes its nb tiles
+            if (prev_n > 0) {
+                if (FLOW == 2) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                if (lane < prev_n)
+                    __hip_atomic_store(prev_flag + (int64_t)lane * f.ntx, prev_val, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (lane == 0) item_sh = atomicAdd(f.head, 1u);
+        }
         __syncthreads();
         // uniform: scalar registers, scalar arithmetic
         const uint32_t item = __builtin_amdgcn_readfirstlane(item_sh);
         if ((int64_t)item >= f.items) return;  // the whole workgroup leaves
         if (LIFE_WG_TRACE && traced < 4) wg_trace(1 + 3 * traced);
         const uint32_t ntx = (uint32_t)f.ntx, nty = (uint32_t)f.nty;
-        const uint32_t p = item / (uint32_t)tiles, k = item - p * (uint32_t)tiles;
-        const uint32_t kr = k / ntx;
-        const int64_t tx = k - kr * ntx, ty = (kr + p) % nty;
+        uint32_t p;
+        int64_t tx, ty;
+        int nb = 1;  // tile rows of this item (a banded item: up to B)
+        if (!BAND) {
+            p = item / (uint32_t)tiles;
+            const uint32_t k = item - p * (uint32_t)tiles, kr = k / ntx;
+            tx = k - kr * ntx;
+            ty = (kr + p) % nty;
+        } else {
+            p = item / (uint32_t)f.per_pass;
+            const uint32_t k = item - p * (uint32_t)f.per_pass;
+            const uint32_t nfull = ntx - 1, G1 = nfull * (uint32_t)f.B + 1u;
+            const uint32_t g = k / G1, off = k - g * G1;
+            const int64_t ty0 = (int64_t)((g + p) % (uint32_t)f.ngroups) * f.B;  // groups rotate per pass
+            if (off < nfull * (uint32_t)f.B) {
+                tx = off % nfull;
+                ty = ty0 + off / nfull;
+            } else {
+                tx = a.bcol;
+                ty = ty0;
+                nb = (int)(f.nty - ty0 < f.B ? f.nty - ty0 : f.B);
+            }
+            if (ty >= f.nty) {  // a padding item of the last group
+                prev_n = 0;
+                prev_flag = nullptr;
+                __syncthreads();  // item_sh is rewritten by the next pull
+                continue;
+            }
+        }
         if (p > 0 && threadIdx.x < 64) {
-            // 15 lanes: tile rows ty-2..ty+2 x columns tx-1..tx+1
+            // tile rows ty-2 .. ty+nb+1 x columns tx-1..tx+1 (one lane each)
             bool ok = true;
             const unsigned int *flag = nullptr;
-            if (lane < 15) {
+            if (lane < 3 * (nb + 4)) {
                 const int64_t dy = lane / 3 - 2, dx = lane % 3 - 1;
                 int64_t yy = (ty + dy) % f.nty, xx = (tx + dx) % f.ntx;
                 if (yy < 0) yy += f.nty;
@@ -866,12 +912,16 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tflow_kernel(FArgs f)
         if (LIFE_WG_TRACE && traced < 4) wg_trace(2 + 3 * traced);
         const uint8_t *in = (p & 1) ? a.out : a.in;
         uint8_t *out = const_cast<uint8_t *>((p & 1) ? a.in : a.out);
-        tile_body_bit<R, WRAPX, WRAPY, FLOW, NW>(a, in, out, tx, ty, xch);
+        if (BAND && tx == a.bcol)
+            tile_body_bit<R, WRAPX, WRAPY, FLOW, NW, true>(a, in, out, tx, ty, xch, a.gsh, nb);
+        else
+            tile_body_bit<R, WRAPX, WRAPY, FLOW, NW>(a, in, out, tx, ty, xch);
         if (!(LIFE_FLOW_EXP & 4)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
         __syncthreads();
         if (LIFE_WG_TRACE && traced < 4) wg_trace(3 + 3 * traced++);
         prev_flag = f.done + ty * f.ntx + tx;
         prev_val = p + 1;
+        prev_n = nb;
     }
 }
 
@@ -1215,25 +1265,44 @@ __device__ __forceinline__ void copy32(uint8_t *dst, const uint8_t *src) {
     for (int k = 0; k < 32; ++k) dst[k] = src[k];
 }
 
+// Threads [h, h + 4K) of a corner exchange (temporal layouts, K = ya): the
+// owned row a send-slot corner c comes from -- c = 0, 1 (SE, SW): the bottom
+// K rows; c = 2, 3 (NE, NW): the top K -- and whether it is the right
+// column (c even) or pair 0 / the first 32 cells (c odd).  The receive slot
+// c lands in apron row -K + r (c = 0, 1) or h + r (c = 2, 3), x-apron left
+// (c even) or right (c odd).
 __global__ void pack_columns_kernel(const uint8_t *buf, int64_t pitch, int64_t ya, int64_t xoff, int64_t w,
-                                    int64_t h, int64_t xa, uint8_t *stage, bool bit) {
-    const int64_t y = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (y >= h) return;
+                                    int64_t h, int64_t xa, uint8_t *stage, bool bit, int64_t nc) {
+    int64_t y = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (y >= h + nc) return;
+    bool right = true, left = true;  // columns: both (slot y and slot h + y)
+    int64_t out = y, lo = h + y;     // the stage entries of the right column and of pair 0 / cells [0, 32)
+    if (y >= h) {                    // corner c, row r: one entry
+        const int64_t c = (y - h) / ya, r = (y - h) % ya;
+        out = lo = y + h;  // entries 2h + cK + r
+        right = (c & 1) == 0;
+        left = !right;
+        y = c < 2 ? h - ya + r : r;
+    }
     const uint8_t *row = buf + (y + ya) * pitch;
     if (xa == 64 && bit) {
         const uint32_t *wd = reinterpret_cast<const uint32_t *>(row + xoff);
         uint64_t *st = reinterpret_cast<uint64_t *>(stage);
-        const uint2 r = pair_of(right_column_bits(wd, w));
-        st[y] = (uint64_t)r.x | ((uint64_t)r.y << 32);
-        st[h + y] = *reinterpret_cast<const uint64_t *>(wd);  // pair 0
+        if (right) {
+            const uint2 r = pair_of(right_column_bits(wd, w));
+            st[out] = (uint64_t)r.x | ((uint64_t)r.y << 32);
+        }
+        if (left) st[lo] = *reinterpret_cast<const uint64_t *>(wd);  // pair 0
         return;
     }
     if (xa == 32) {  // 32 byte cells per row and side
-        copy32(stage + 32 * y, row + xoff + w - 32);
-        const uint4 *l = reinterpret_cast<const uint4 *>(row + xoff);
-        uint4 *st = reinterpret_cast<uint4 *>(stage + 32 * (h + y));
-        st[0] = l[0];
-        st[1] = l[1];
+        if (right) copy32(stage + 32 * out, row + xoff + w - 32);
+        if (left) {
+            const uint4 *l = reinterpret_cast<const uint4 *>(row + xoff);
+            uint4 *st = reinterpret_cast<uint4 *>(stage + 32 * lo);
+            st[0] = l[0];
+            st[1] = l[1];
+        }
         return;
     }
     stage[y] = (uint8_t)get_cell(row, xoff, w - 1, bit);
@@ -1241,24 +1310,37 @@ __global__ void pack_columns_kernel(const uint8_t *buf, int64_t pitch, int64_t y
 }
 
 __global__ void unpack_columns_kernel(uint8_t *buf, int64_t pitch, int64_t ya, int64_t xoff, int64_t w,
-                                      int64_t h, int64_t xa, const uint8_t *stage, bool bit) {
-    const int64_t y = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (y >= h) return;
+                                      int64_t h, int64_t xa, const uint8_t *stage, bool bit, int64_t nc) {
+    int64_t y = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (y >= h + nc) return;
+    bool left = true, right = true;  // columns: slot y -> left apron, slot h + y -> right apron
+    int64_t in = y, ri = h + y;
+    if (y >= h) {  // corner c, row r: apron rows -K + r (c < 2) or h + r, left apron for even c
+        const int64_t c = (y - h) / ya, r = (y - h) % ya;
+        in = ri = y + h;
+        left = (c & 1) == 0;
+        right = !left;
+        y = c < 2 ? r - ya : h + r;
+    }
     uint8_t *row = buf + (y + ya) * pitch;
     if (xa == 64 && bit) {
         uint32_t *wd = reinterpret_cast<uint32_t *>(row + xoff);
         const uint64_t *st = reinterpret_cast<const uint64_t *>(stage);
-        reinterpret_cast<uint64_t *>(wd)[-1] = st[y];  // pair -1 = cells [-64, 0)
-        const uint64_t r = st[h + y];
-        put_right_apron_bits(wd, w, nat64((uint32_t)r, (uint32_t)(r >> 32)));
+        if (left) reinterpret_cast<uint64_t *>(wd)[-1] = st[in];  // pair -1 = cells [-64, 0)
+        if (right) {
+            const uint64_t r = st[ri];
+            put_right_apron_bits(wd, w, nat64((uint32_t)r, (uint32_t)(r >> 32)));
+        }
         return;
     }
     if (xa == 32) {
-        uint4 *l = reinterpret_cast<uint4 *>(row + xoff - 32);
-        const uint4 *st = reinterpret_cast<const uint4 *>(stage + 32 * y);
-        l[0] = st[0];
-        l[1] = st[1];
-        copy32(row + xoff + w, stage + 32 * (h + y));
+        if (left) {
+            uint4 *l = reinterpret_cast<uint4 *>(row + xoff - 32);
+            const uint4 *st = reinterpret_cast<const uint4 *>(stage + 32 * in);
+            l[0] = st[0];
+            l[1] = st[1];
+        }
+        if (right) copy32(row + xoff + w, stage + 32 * ri);
         return;
     }
     set_cell(row, xoff, -1, stage[y] ? 1u : 0u, bit);
@@ -1528,6 +1610,8 @@ Tunings &tunings() {
 // one alternative each: every other shape measured slower at 65536^2
 // (profiles/r02/r2w, r03/r4g) and at 32768^2 (bit 32x8, 24x12, 16x16:
 // 0.96-0.99 of 24x8, profiles/r05/a).
+// (byte 64-row tiles, round 5: 61.3 vs 60.5 T at 65536^2, 48.1 vs 50.0 T at
+// 32768^2 -- flat, removed; profiles/r05/g)
 bool temporal_rows_ok(bool bit, int nr) { return bit ? (nr == 16 || nr == 24) : (nr == 32 || nr == 48); }
 // bit tile shapes with a kernel instance (pair rows R x waves NW)
 bool bit_shape_ok(int R, int NW) { return NW == 8 && (R == 16 || R == 24); }
@@ -1904,18 +1988,39 @@ hipError_t launch_tstep(const life_layout &Lin, const uint8_t *in, uint8_t *out,
 namespace {
 // Instances of the dataflow tiles (bit, both axes wrapped): one per tile shape
 // and hand-off form.
-const void *flow_kernel_of(const life_layout &L, int flow) {
+// (LIFE_FLOW_BANDS=0: full-width tiles in the last column; A/B knob)
+bool flow_bands_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("LIFE_FLOW_BANDS");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return on;
+}
+const void *flow_kernel_of(const life_layout &L, int flow, bool band = false) {
     if (!is_bit(L)) return nullptr;
     const int R = temporal_rows(true), NW = tile_waves(true);
-#define LIFE_BIT_CASE(r, nw)                                                                \
-    if (R == r && NW == nw)                                                                 \
-        return flow == 2 ? (const void *)tflow_kernel<r, true, true, 2, nw>                 \
-                         : (const void *)tflow_kernel<r, true, true, 1, nw>;
+#define LIFE_BIT_CASE(r, nw)                                                                     \
+    if (R == r && NW == nw) {                                                                    \
+        if (band)                                                                                \
+            return flow == 2 ? (const void *)tflow_kernel<r, true, true, 2, nw, true>            \
+                             : (const void *)tflow_kernel<r, true, true, 1, nw, true>;           \
+        return flow == 2 ? (const void *)tflow_kernel<r, true, true, 2, nw>                      \
+                         : (const void *)tflow_kernel<r, true, true, 1, nw>;                     \
+    }
     LIFE_BIT_SHAPES(LIFE_BIT_CASE)
 #undef LIFE_BIT_CASE
     return nullptr;
 }
+// the banded form for this geometry: a banded last column (tile_geom)
+bool flow_band(const TileGeom &g) { return g.gsh < 6 && flow_bands_enabled(); }
 }  // namespace
+
+int64_t flow_items_per_pass(const life_layout &L, int m) {
+    const TileGeom g = tile_geom(L, m);
+    if (!flow_band(g)) return g.ntx * g.nty;
+    const int64_t B = 64 >> g.gsh, ngroups = (g.nty + B - 1) / B;
+    return ngroups * ((g.ntx - 1) * B + 1);
+}
 
 bool flow_ok(const life_layout &L, int m) {
     // an instance for this encoding / tile shape, and the dependency rule
@@ -1953,11 +2058,16 @@ hipError_t launch_tflow(const life_layout &L, const uint8_t *in, uint8_t *out, i
     f.t.h = L.h;
     f.t.ya = L.yapron;
     f.t.m = m;
-    f.t.gsh = 6;  // no banded column in the dataflow form
-    f.t.bcol = -1;
+    const bool band = flow_band(g);
+    if (band) fn = flow_kernel_of(L, flow, true);
+    f.t.gsh = band ? (int32_t)g.gsh : 6;
+    f.t.bcol = band ? g.bcol : -1;
     f.ntx = g.ntx;
     f.nty = g.nty;
-    f.items = passes * g.ntx * g.nty;
+    f.B = band ? 64 >> g.gsh : 1;
+    f.ngroups = (g.nty + f.B - 1) / f.B;
+    f.per_pass = flow_items_per_pass(L, m);
+    f.items = passes * f.per_pass;
     f.head = head;
     f.done = done;
     hipError_t e = hipMemsetAsync(head, 0, sizeof(unsigned int), s);  // the error word is the caller's
@@ -2093,9 +2203,12 @@ hipError_t launch_small(const life_layout &L, const uint8_t *in, uint8_t *out, i
     return hipGetLastError();
 }
 
-hipError_t launch_pack_columns(const life_layout &L, const uint8_t *buf, uint8_t *stage, hipStream_t s) {
-    pack_columns_kernel<<<blocks_for(L.h, 256), 256, 0, s>>>(buf, L.pitch, L.yapron, L.xoff, L.w, L.h, L.xapron,
-                                                              stage, is_bit(L));
+hipError_t launch_pack_columns(const life_layout &L, const uint8_t *buf, uint8_t *stage, hipStream_t s,
+                               bool corners) {
+    if (corners && L.xapron < 32) return hipErrorInvalidValue;
+    const int64_t nc = corners ? 4 * L.yapron : 0;
+    pack_columns_kernel<<<blocks_for(L.h + nc, 256), 256, 0, s>>>(buf, L.pitch, L.yapron, L.xoff, L.w, L.h, L.xapron,
+                                                                   stage, is_bit(L), nc);
     return hipGetLastError();
 }
 
@@ -2105,9 +2218,12 @@ hipError_t launch_wrap_columns(const life_layout &L, uint8_t *buf, hipStream_t s
     return hipGetLastError();
 }
 
-hipError_t launch_unpack_columns(const life_layout &L, uint8_t *buf, const uint8_t *stage, hipStream_t s) {
-    unpack_columns_kernel<<<blocks_for(L.h, 256), 256, 0, s>>>(buf, L.pitch, L.yapron, L.xoff, L.w, L.h,
-                                                                L.xapron, stage, is_bit(L));
+hipError_t launch_unpack_columns(const life_layout &L, uint8_t *buf, const uint8_t *stage, hipStream_t s,
+                                 bool corners) {
+    if (corners && L.xapron < 32) return hipErrorInvalidValue;
+    const int64_t nc = corners ? 4 * L.yapron : 0;
+    unpack_columns_kernel<<<blocks_for(L.h + nc, 256), 256, 0, s>>>(buf, L.pitch, L.yapron, L.xoff, L.w, L.h,
+                                                                     L.xapron, stage, is_bit(L), nc);
     return hipGetLastError();
 }
 

@@ -185,7 +185,7 @@ int life::halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int 
     if (rc != LIFE_OK) return rc;
     const int c0 = L.coords[0], c1 = L.coords[1];
     const int64_t w = L.w, h = L.h, xa = L.xapron, ya = L.yapron;
-    life_halo_op tmp[10];
+    life_halo_op tmp[16];
     int n = 0;
     auto add = [&](int phase, int kind, int peer, int what, int64_t index, int64_t width, int64_t first,
                    int64_t count) {
@@ -199,8 +199,25 @@ int life::halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int 
         o.first = first;
         o.count = count;
     };
+    const bool px = dims0 > 1 || loop, py = dims1 > 1 || loop;
+    // Both axes exchanged by messages with K-deep temporal aprons: ONE phase
+    // (one RCCL group per exchange instead of two back to back, round 5):
+    // columns, whole padded rows (their x-apron bytes are stale and are
+    // overwritten), and the four K x xapron corners explicitly, as
+    // life_cart.c:257-273 exchanges them (there one cell each).  Sends go in
+    // direction order E, W, S, N, SE, SW, NE, NW; each receive is listed in
+    // the order of the direction its sender sends in, so the k-th message
+    // between two ranks pairs up however many directions they share (dims 2,
+    // the loopback's self).  Corners are received into staging and unpacked
+    // after the group, over the stale row bytes.  Not for the loopback (the
+    // shard its own peer in all eight directions): RCCL ran the sixteen
+    // self-messages of one group in 39 us, longer than the two groups of the
+    // column and row phases (19 + 14 us; 16384 x 32768, profiles/r05/g),
+    // while distinct peers over xGMI are served by separate channels.
+    const bool fused = px && py && L.generations_per_exchange > 1 && !loop;
+    const int ph_rows = fused ? 0 : 1;
     // Phase 0: columns (dim 0 splits x), owned rows only.  MPI_Cart_shift(dim 0).
-    if (dims0 == 1 && !loop) {
+    if (!px) {
         add(0, LIFE_HALO_FILL, -1, LIFE_HALO_COLUMN, -xa, xa, ya, h);
     } else {
         const int right = cart_rank((c0 + 1) % dims0, c1, dims1);
@@ -211,17 +228,36 @@ int life::halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int 
         add(0, LIFE_HALO_RECV, left, LIFE_HALO_COLUMN, -xa, xa, ya, h);
         add(0, LIFE_HALO_RECV, right, LIFE_HALO_COLUMN, w, xa, ya, h);
     }
-    // Phase 1: whole rows including the x-apron just received (the corners).
-    if (dims1 == 1 && !loop) {
+    // Phase 1 (phase 0 when fused): whole rows including the x-apron just
+    // received (the corners), or with a stale x-apron the corners overwrite.
+    if (!py) {
         add(1, LIFE_HALO_FILL, -1, LIFE_HALO_ROW, 0, ya, -xa, w + 2 * xa);
     } else {
         const int right = cart_rank(c0, (c1 + 1) % dims1, dims1);
         const int left = cart_rank(c0, (c1 - 1 + dims1) % dims1, dims1);
         // life_cart.c:235-238 order.  Padded row of owned row y is y + ya.
-        add(1, LIFE_HALO_SEND, right, LIFE_HALO_ROW, h, ya, -xa, w + 2 * xa);
-        add(1, LIFE_HALO_SEND, left, LIFE_HALO_ROW, ya, ya, -xa, w + 2 * xa);
-        add(1, LIFE_HALO_RECV, left, LIFE_HALO_ROW, 0, ya, -xa, w + 2 * xa);
-        add(1, LIFE_HALO_RECV, right, LIFE_HALO_ROW, h + ya, ya, -xa, w + 2 * xa);
+        add(ph_rows, LIFE_HALO_SEND, right, LIFE_HALO_ROW, h, ya, -xa, w + 2 * xa);
+        add(ph_rows, LIFE_HALO_SEND, left, LIFE_HALO_ROW, ya, ya, -xa, w + 2 * xa);
+        add(ph_rows, LIFE_HALO_RECV, left, LIFE_HALO_ROW, 0, ya, -xa, w + 2 * xa);
+        add(ph_rows, LIFE_HALO_RECV, right, LIFE_HALO_ROW, h + ya, ya, -xa, w + 2 * xa);
+    }
+    if (fused) {
+        // direction d = (dx, dy) in the order SE, SW, NE, NW; the shard at
+        // (c0 + dx, c1 + dy) gets my corner next to it: x side by dx (my right
+        // column w - xa, or cells [0, xa)), rows by dy (my bottom K rows,
+        // padded h, or my top K, padded ya)
+        static const int kDir[4][2] = {{1, 1}, {-1, 1}, {1, -1}, {-1, -1}};
+        auto at = [&](int dx, int dy) {
+            return cart_rank((c0 + dx + dims0) % dims0, (c1 + dy + dims1) % dims1, dims1);
+        };
+        for (const auto &d : kDir)
+            add(0, LIFE_HALO_SEND, at(d[0], d[1]), LIFE_HALO_CORNER, d[0] > 0 ? w - xa : 0, xa, d[1] > 0 ? h : ya,
+                ya);
+        // the sender of direction d sits at -d: its corner lands in my apron
+        // on the side facing it (left apron -xa when it is left of me)
+        for (const auto &d : kDir)
+            add(0, LIFE_HALO_RECV, at(-d[0], -d[1]), LIFE_HALO_CORNER, d[0] > 0 ? -xa : w, xa,
+                d[1] > 0 ? 0 : h + ya, ya);
     }
     if (ops) {
         if (max_ops < n) return LIFE_EINVAL;

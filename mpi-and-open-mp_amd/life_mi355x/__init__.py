@@ -40,7 +40,7 @@ KERNEL_BIT = 1
 KERNELS = {"byte": KERNEL_BYTE, "bit": KERNEL_BIT}
 XPORT_AUTO, XPORT_RCCL, XPORT_LOCAL = 0, 1, 2
 HALO_SEND, HALO_RECV, HALO_FILL = 0, 1, 2
-HALO_COLUMN, HALO_ROW = 0, 1
+HALO_COLUMN, HALO_ROW, HALO_CORNER = 0, 1, 2
 OPT_SMALL_GRID, OPT_OVERLAP, OPT_SMALL_WINDOW, OPT_BLOCK_GENS, OPT_LOOPBACK, OPT_FLOW = 1, 2, 4, 5, 6, 7
 OPT_FLOW_CHUNK = 8
 OPT_DEEP_HALO = 9
@@ -295,8 +295,9 @@ class Life:
             self.configure(OPT_SMALL_WINDOW, int(window[0]) * 256 + int(window[1]))
         if not overlap:
             self.configure(OPT_OVERLAP, 0)
-        # flow: None (library default: the dataflow tiles where they apply),
-        # or a LIFE_OPT_FLOW value (0: one launch per pass)
+        # flow: None (library default 3: the dataflow tiles where a pass is
+        # only a few rounds of workgroups), or a LIFE_OPT_FLOW value (0: one
+        # launch per pass)
         if flow is not None:
             self.configure(OPT_FLOW, int(flow))
 

@@ -4,7 +4,9 @@ transport issues, matched in issue order per peer like ncclSend/ncclRecv) on
 apron-padded blocks, step each block with the oracle, and must reproduce
 the single-grid oracle bit for bit.  This is the N>1 path of
 life_dev_step minus the device: partition, neighbour table, op order,
-corner propagation through width+2 rows."""
+corners through width+2 rows (one-cell aprons) or as explicit K x xapron
+blocks of the one-phase plan (temporal aprons, both axes partitioned), whose
+receives land after the rows' stale apron bytes."""
 import os
 import socket
 import sys
@@ -46,13 +48,15 @@ def _worker(rank, world, port, nx, ny, dims, gens, seed, kernel, q):
 
         def region(o):
             _, _, _, what, index, first, count, width = o
-            if what == lm.HALO_COLUMN:
+            if what in (lm.HALO_COLUMN, lm.HALO_CORNER):
                 return (slice(first, first + count), slice(index + xa, index + xa + width))
             return (slice(index, index + width), slice(first + xa, first + xa + count))
 
         def exchange():
             for phase in (0, 1):
                 ops = [o for o in plan if o[0] == phase]
+                if not ops:  # the fused one-phase plan (both axes, temporal aprons)
+                    continue
                 if ops[0][1] == lm.HALO_FILL:  # axis inside the shard: periodic wrap
                     if phase == 0:
                         P[ya:ya + h, :] = P[ya:ya + h, xa + np.arange(-xa, w + xa) % w]

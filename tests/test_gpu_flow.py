@@ -17,8 +17,14 @@ pytestmark = pytest.mark.gpu
 # (2048 x 8000: 24 tile rows, the rotation wraps several times per call;
 # 4032 = 63 pairs: a second tile column owning one pair)
 # (a call takes the dataflow form from 4 passes on)
+# A last tile column owning o <= 30 pairs runs as banded items of 64 / G tile
+# rows (G = 2^ceil(log2(o + 2)) lanes), the rows padded to whole groups:
+# 4096 / 4032 / 128 / 64 (G = 4, 16 rows per item), 8192 (o = 4, G = 8),
+# 16384 (o = 8, G = 16, 4 rows: the configs[3] N = 8 block's width), 32768
+# wide in test_flow_fullsize_census (o = 16, G = 32).
 CASES = [(2048, 1000, 87, 20), (1024, 3000, 64, 16), (4096, 1100, 43, 10), (1984, 700, 135, 32), (64, 900, 37, 8),
-         (2112, 2000, 61, 12), (128, 2048, 85, 20), (2048, 8000, 81, 20), (4032, 600, 90, 21)]
+         (2112, 2000, 61, 12), (128, 2048, 85, 20), (2048, 8000, 81, 20), (4032, 600, 90, 21),
+         (8192, 3000, 61, 12), (16384, 1500, 50, 12)]
 
 
 @pytest.mark.parametrize("flow", [1, 2])

@@ -128,32 +128,52 @@ def test_layout_rejects_empty_blocks(lm):
                                         (9, 9, (3, 3)), (5, 5, (1, 1)), (100, 3, (4, 3)), (256, 64, (2, 2)),
                                         (512, 80, (4, 2)), (64, 40, (1, 4)), (256, 9, (4, 1))])
 def test_halo_plan_is_symmetric(lm, kernel, nx, ny, dims):
-    """Every recv has a matching send at the peer: same phase, same shape,
-    matched in issue order (RCCL p2p semantics), and sends go to the Cartesian
-    neighbour whose apron they fill."""
+    """Every recv has a matching send at the peer: same phase, same kind of
+    message and shape, matched in issue order (RCCL p2p semantics), and sends
+    go to the Cartesian neighbour whose apron they fill.  Both axes
+    partitioned with temporal (K-deep) aprons: ONE phase -- columns, rows and
+    the four corner blocks (life_cart.c:257-273) -- instead of columns, then
+    rows of width + 2 that carry the corners."""
     world = dims[0] * dims[1]
     plans = {r: lm.halo_plan(nx, ny, dims, r, kernel) for r in range(world)}
     lay = {r: lm.layout_query(nx, ny, dims, r, kernel) for r in range(world)}
     for r, ops in plans.items():
-        xa, ya = lay[r].xapron, lay[r].yapron
-        for phase in (0, 1):
-            ph = [o for o in ops if o[0] == phase]
-            if dims[phase] == 1:
-                assert [o[1] for o in ph] == [lm.HALO_FILL]
+        L = lay[r]
+        xa, ya, c0, c1 = L.xapron, L.yapron, L.coords[0], L.coords[1]
+        fused = dims[0] > 1 and dims[1] > 1 and L.generations_per_exchange > 1
+        kinds = {ph: [(o[1], o[3]) for o in ops if o[0] == ph] for ph in (0, 1)}
+        S, R, F = lm.HALO_SEND, lm.HALO_RECV, lm.HALO_FILL
+        C, W, X = lm.HALO_COLUMN, lm.HALO_ROW, lm.HALO_CORNER
+        if fused:
+            assert kinds[1] == []
+            assert kinds[0] == [(S, C), (S, C), (R, C), (R, C), (S, W), (S, W), (R, W), (R, W)] + \
+                [(S, X)] * 4 + [(R, X)] * 4
+        else:
+            for ph, what in ((0, C), (1, W)):
+                want = [(F, what)] if dims[ph] == 1 else [(S, what), (S, what), (R, what), (R, what)]
+                assert kinds[ph] == want
+        for o in ops:
+            if o[1] != R:
                 continue
-            assert [o[1] for o in ph] == [lm.HALO_SEND, lm.HALO_SEND, lm.HALO_RECV, lm.HALO_RECV]
-            for o in (o for o in ph if o[1] == lm.HALO_RECV):
-                peer = o[2]
-                kth = [q for q in ph if q[1] == lm.HALO_RECV and q[2] == peer].index(o)
-                s_ = [q for q in plans[peer] if q[0] == phase and q[1] == lm.HALO_SEND and q[2] == r][kth]
-                assert (s_[6], s_[7]) == (o[6], o[7])  # same cells x rows
-                if phase == 0:  # x-apron <- the peer's edge columns
-                    assert o[7] == xa
-                    assert (o[4], s_[4]) in ((-xa, lay[peer].w - xa), (lay[r].w, 0))
-                else:  # y-apron rows <- the peer's edge rows (padded row = owned + yapron)
-                    assert o[7] == ya
-                    assert (o[4], s_[4]) in ((0, lay[peer].h), (lay[r].h + ya, ya))
-
+            peer, ph = o[2], o[0]
+            kth = [q for q in ops if q[0] == ph and q[1] == R and q[2] == peer].index(o)
+            s_ = [q for q in plans[peer] if q[0] == ph and q[1] == S and q[2] == r][kth]
+            P = lay[peer]
+            assert (s_[3], s_[6], s_[7]) == (o[3], o[6], o[7])  # same kind of message, cells x rows
+            dx = dy = 0
+            if o[3] in (C, X):  # x-apron <- the peer's edge columns
+                assert o[7] == xa
+                assert (o[4], s_[4]) in ((-xa, P.w - xa), (L.w, 0))
+                dx = -1 if o[4] < 0 else 1
+            if o[3] == W:  # y-apron rows <- the peer's edge rows (padded row = owned + yapron)
+                assert o[7] == ya
+                assert (o[4], s_[4]) in ((0, P.h), (L.h + ya, ya))
+                dy = -1 if o[4] == 0 else 1
+            if o[3] == X:  # corner: K rows of the peer's top / bottom edge into the top / bottom apron
+                assert o[6] == ya
+                assert (o[5], s_[5]) in ((0, P.h), (L.h + ya, ya))
+                dy = -1 if o[5] == 0 else 1
+            assert tuple(P.coords) == ((c0 + dx) % dims[0], (c1 + dy) % dims[1])
 
 @pytest.mark.parametrize("nx,ny,dims,wide", [(65536, 65536, (1, 1), True), (262144, 131072, (4, 2), True),
                                              (1000, 37, (1, 1), True), (31, 37, (1, 1), False),
