@@ -1268,7 +1268,8 @@ static int step_flow(life_dev *d, int64_t generations, int64_t *done) {
             const double cells = (double)L.w * (double)L.h;
             d->acc_bytes += (double)n * cells * 0.25;
             d->acc_updates += (double)n * cells * (double)m;
-            d->acc_valu += (double)n * (double)tiles * 64.0 * life::tstep_valu_per_tile_lane(m, false);
+            d->acc_valu += (double)n * (double)life::flow_items_per_pass(L, m, true) * 64.0 *
+                           life::tstep_valu_per_tile_lane(m, false);
         }
         if (n & 1) s.cur ^= 1;
         left -= n;

@@ -84,8 +84,10 @@ constexpr int64_t kTemporalSlackRows = 8 * 96;
 // Pass p reads `in` for even p and `out` for odd p: after it, the result is
 // in `out` when passes is odd, else in `in`.
 bool flow_ok(const life_layout &L, int m);
-// work items of one dataflow pass (tiles, or tiles + banded items of a banded last column)
-int64_t flow_items_per_pass(const life_layout &L, int m);
+// work items of one dataflow pass (tiles, or tiles + banded items of a banded
+// last column; the queue also holds no-op items that pad the last group of
+// banded rows unless work_only)
+int64_t flow_items_per_pass(const life_layout &L, int m, bool work_only = false);
 int flow_slots(const life_layout &L);  // resident workgroups of L's dataflow kernel on this device
 int tile_slots(const life_layout &L);  // resident workgroups of L's per-launch tile kernel on this device
 // ev0 / ev1 (optional): events stamped with the kernel dispatch's own start

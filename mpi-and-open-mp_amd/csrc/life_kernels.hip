@@ -359,6 +359,17 @@ struct XchB {
 #ifndef LIFE_FLOW_EXP
 #define LIFE_FLOW_EXP 0
 #endif
+// LIFE_FLOW_BP_AHEAD (default 1): the dataflow tiles' generation loop issues
+// each row's two neighbour permutes that many rows ahead of their use, rows
+// fenced in program order.  Left to itself the compiler scheduled that loop
+// (more live state around it than in tstep_bit_kernel's) with every permute
+// right before its wait: mean permute -> wait distance 1.8 instructions
+// against 7.6-9.8 in the per-launch tiles (tests/test_isa.py), the
+// scheduling loss round 4 measured at 8 % there.  (Forcing the same in the
+// per-launch tiles, whose own schedule is good, cost 1-3.5 %: off there.)
+#ifndef LIFE_FLOW_BP_AHEAD
+#define LIFE_FLOW_BP_AHEAD 1
+#endif
 // LIFE_FAST_WRAP: a tile's wrapped pair column and first row by one
 // conditional add / subtract instead of a 64-bit remainder (per lane for the
 // column) when the axis is long enough for the index to be at most one
@@ -477,6 +488,14 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
             ve[0] = BitEnc::rule1(ae0, ae1, pe0, pe1, ce0, ce1, ve[0]);
             vo[0] = BitEnc::rule1(ao0, ao1, po0, po1, co0, co1, vo[0]);
         }
+        constexpr int BAH = FLOW ? LIFE_FLOW_BP_AHEAD : 0;  // permutes ahead (dataflow tiles only)
+        uint32_t bl[BAH > 0 ? BAH : 1], br[BAH > 0 ? BAH : 1];
+#pragma unroll
+        for (int k = 0; k < BAH; ++k)
+            if (2 + k < R - 1) {
+                bl[k] = bperm(laddr, vo[2 + k]);
+                br[k] = bperm(raddr, ve[2 + k]);
+            }
 #pragma unroll
         for (int r = 1; r < R - 1; ++r) {
             uint32_t ne0, ne1, no0, no1;
@@ -485,6 +504,19 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
                 ne1 = xch[par][wi + 1][5][lane];
                 no0 = xch[par][wi + 1][6][lane];
                 no1 = xch[par][wi + 1][7][lane];
+            } else if (BAH > 0) {
+                const uint32_t l = bl[0], rr = br[0];
+#pragma unroll
+                for (int k = 0; k + 1 < BAH; ++k) {
+                    bl[k] = bl[k + 1];
+                    br[k] = br[k + 1];
+                }
+                if (r + 1 + BAH < R - 1) {
+                    bl[BAH - 1] = bperm(laddr, vo[r + 1 + BAH]);
+                    br[BAH - 1] = bperm(raddr, ve[r + 1 + BAH]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                BitEnc::pair_sums(ve[r + 1], vo[r + 1], l, rr, ne0, ne1, no0, no1);
             } else {
                 hsum(ve[r + 1], vo[r + 1], ne0, ne1, no0, no1);
             }
@@ -2015,11 +2047,12 @@ const void *flow_kernel_of(const life_layout &L, int flow, bool band = false) {
 bool flow_band(const TileGeom &g) { return g.gsh < 6 && flow_bands_enabled(); }
 }  // namespace
 
-int64_t flow_items_per_pass(const life_layout &L, int m) {
+int64_t flow_items_per_pass(const life_layout &L, int m, bool work_only) {
     const TileGeom g = tile_geom(L, m);
     if (!flow_band(g)) return g.ntx * g.nty;
     const int64_t B = 64 >> g.gsh, ngroups = (g.nty + B - 1) / B;
-    return ngroups * ((g.ntx - 1) * B + 1);
+    // work_only: without the no-op padding items of the last group
+    return work_only ? (g.ntx - 1) * g.nty + ngroups : ngroups * ((g.ntx - 1) * B + 1);
 }
 
 bool flow_ok(const life_layout &L, int m) {

@@ -105,10 +105,20 @@ def test_flow_needs_four_passes(gpu, oracle):
         np.testing.assert_array_equal(life.gather(), g)
 
 
-def test_flow_default_off(gpu):
-    """Per-launch tiles are the default (LIFE_OPT_FLOW 0): the pair tiles beat
-    the dataflow form at every pass size (profiles/r03/r4g)."""
+def test_flow_default_automatic(gpu):
+    """The default (LIFE_OPT_FLOW 3) takes the dataflow form when a pass is
+    under 5 rounds of resident workgroups -- the per-launch tiles' tail then
+    idles the chip (32768^2: 2.2 rounds, +8 %, profiles/r05/a) -- and the
+    per-launch tiles at 65536^2 (8.6 rounds, where they win by 3 %)."""
     with gpu.Life(2048, 1000, kernel="bit", small_grid=False) as life:
+        life.fill_random(3, 0.5)
+        life.step(100)
+        assert life.last_path() == "flow"
+    with gpu.Life(65536, 65536, kernel="bit") as life:
+        life.fill_random(3, 0.5)
+        life.step(48)
+        assert life.last_path() == "tiles"
+    with gpu.Life(2048, 1000, kernel="bit", small_grid=False, flow=0) as life:
         life.fill_random(3, 0.5)
         life.step(100)
         assert life.last_path() == "tiles"
@@ -117,7 +127,7 @@ def test_flow_default_off(gpu):
 def test_flow_rejected_options(gpu):
     with gpu.Life(256, 256, kernel="bit") as life:
         with pytest.raises(RuntimeError):
-            life.configure(gpu.OPT_FLOW, 3)
+            life.configure(gpu.OPT_FLOW, 4)
         with pytest.raises(RuntimeError):
             life.configure(gpu.OPT_FLOW_CHUNK, -1)
         with pytest.raises(RuntimeError):  # the byte dataflow form (value | 4) was removed

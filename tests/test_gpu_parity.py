@@ -123,11 +123,11 @@ def test_timing_stats(gpu, kernel, nx, gens, flow):
                 ghost = m if kernel == "bit" else K  # byte tiles: compile-time ghost depth K
                 nty = -(-4096 // (NW * R - 2 * ghost))
                 if kernel == "bit":
-                    # 64 pairs per row: two tile columns, the second owning 2 pairs; per-launch tiles run it as
-                    # bands of 4 lanes, 16 tile rows per workgroup (life_kernels.hip tile_geom / region_items;
-                    # not in the dataflow form)
+                    # 64 pairs per row: two tile columns, the second owning 2 pairs; it runs as bands of 4
+                    # lanes, 16 tile rows per workgroup (life_kernels.hip tile_geom / region_items; the dataflow
+                    # form's banded items likewise, its no-op padding items not counted)
                     tiles = 2 * nty
-                    if not flow and os.environ.get("LIFE_BANDS", "1") != "0":
+                    if os.environ.get("LIFE_FLOW_BANDS" if flow else "LIFE_BANDS", "1") != "0":
                         tiles = nty + -(-nty // 16)
                     per_row = 22 * m  # a pair row: 2 v_alignbit + 2 full adders + 2 rules
                 else:  # 128 words per row: three tile columns; drifting frame 12 VALU + pack/unpack 35
@@ -443,5 +443,6 @@ def test_deep_halo_exchange_count(gpu, oracle, rccl):
             life.step(20)
             assert life.phase_stats()["blocks"] == blocks
             np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, 25, threads=4))
+
 
 

@@ -124,3 +124,29 @@ def test_byte_permutes_issued_ahead(isa):
     for body in loops:
         ahead = sum(1 for t in body if t == "s_waitcnt lgkmcnt(2)")
         assert ahead >= 40, f"{ahead} waits with two permutes in flight"
+
+
+FLOW_KERNEL = "tflow_kernel<24, true, true, 1, 8, false>"  # the dataflow form (write-through hand-off)
+
+
+def test_flow_permutes_issued_ahead(isa):
+    """The dataflow tiles' generation loop issues each row's two permutes one
+    row ahead (LIFE_FLOW_BP_AHEAD = 1): its waits leave the next row's two
+    (and the current row's second) in flight -- lgkmcnt(2) / (3).  Left to
+    the compiler, every permute sat right before its wait there (mean
+    distance 1.8 instructions against 7.6-9.8 in the per-launch tiles)."""
+    lines = kernel_lines(isa[0], FLOW_KERNEL)
+    loops = []
+    for addr, op, text in lines:
+        m = re.match(r"s_cbranch_\w+ (\d+)$", text)
+        if not m or int(m.group(1)) < 0x8000:
+            continue
+        target = addr + 4 + 4 * (int(m.group(1)) - 0x10000)
+        body = [t for a, _, t in lines if target <= a <= addr]
+        ops = [t.split()[0] for t in body]
+        if "s_barrier" in ops and ops.count("v_bitop3_b32") == 480:
+            loops.append(body)
+    assert loops, "no dataflow generation loop found"
+    for body in loops:
+        ahead = sum(1 for t in body if t in ("s_waitcnt lgkmcnt(2)", "s_waitcnt lgkmcnt(3)"))
+        assert ahead >= 40, f"{ahead} waits with permutes of the next row in flight"
