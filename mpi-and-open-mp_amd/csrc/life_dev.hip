@@ -248,18 +248,6 @@ int alloc_fill_byte() {
     return e && atoi(e) != 0 ? 0xA5 : 0;
 }
 
-// CUs per XCD kept free of the interior tiles of the overlapped schedule
-// (LIFE_COMM_CUS, read at each life_dev_create*; default 0): the interior
-// stream is created with a CU mask without the top k CUs of every 32-CU mask
-// word (one word per XCD on MI355X), so the halo's pack / RCCL / unpack
-// kernels, queued behind the ring on the comm stream, find free CUs at once
-// instead of waiting for interior tiles to retire.
-int comm_cus() {
-    const char *e = getenv("LIFE_COMM_CUS");
-    const int v = e ? atoi(e) : 0;
-    return v >= 0 && v <= 16 ? v : 0;
-}
-
 int shard_alloc(life_dev *d, Shard &s) {
     HIPCHK(hipSetDevice(s.device));
     // The streams first: every fill below is ordered on the stream that later
@@ -271,23 +259,7 @@ int shard_alloc(life_dev *d, Shard &s) {
     HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
     const bool prio = stream_priorities();
     HIPCHK(hipStreamCreateWithPriority(&s.stream, hipStreamNonBlocking, prio ? prio_hi : 0));
-    if (const int k = comm_cus()) {
-        int cus = 0;
-        HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s.device));
-        std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0xFFFFFFFFu);
-        if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
-        for (uint32_t &w : mask) {
-            const int n = __builtin_popcount(w);
-            for (int b = 31, cut = 0; b >= 0 && cut < k && n - cut > 1; --b)
-                if (w >> b & 1u) {
-                    w &= ~(1u << b);
-                    ++cut;
-                }
-        }
-        HIPCHK(hipExtStreamCreateWithCUMask(&s.stream2, (uint32_t)mask.size(), mask.data()));
-    } else {
-        HIPCHK(hipStreamCreateWithPriority(&s.stream2, hipStreamNonBlocking, prio ? prio_lo : 0));
-    }
+    HIPCHK(hipStreamCreateWithPriority(&s.stream2, hipStreamNonBlocking, prio ? prio_lo : 0));
     HIPCHK(hipStreamCreateWithPriority(&s.comm_stream, hipStreamNonBlocking, prio ? prio_hi : 0));
     const int fill = alloc_fill_byte();
     const int64_t slack = s.lay.generations_per_exchange > 1 ? life::kTemporalSlackRows : 0;
@@ -727,6 +699,7 @@ int phase_end(life_dev *d, const std::vector<PhaseEvents *> &pe, const std::vect
         Shard &s = d->shards[si];
         HIPCHK(hipSetDevice(s.device));
         if (pe[si]) HIPCHK(hipEventRecord(pe[si]->halo1, s.stream));
+        // (priorities belong to the stream roles: no swap then)
         if (halo_side[si] || stream_priorities()) {
             HIPCHK(hipEventRecord(s.ev_int, s.stream2));
             HIPCHK(hipStreamWaitEvent(s.stream, s.ev_int, 0));
