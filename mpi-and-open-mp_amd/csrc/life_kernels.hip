@@ -1876,13 +1876,30 @@ static bool xcd_order_byte_enabled() {
     return on;
 }
 
-// LIFE_TAIL_SPLIT=0: no half-height tail tiles (A/B knob)
-static bool tail_split_enabled() {
-    static const bool on = [] {
+// LIFE_TAIL_SPLIT: 0 no half-height tail tiles, 1 the round-4 rule (the
+// fewest bottom tile rows whose half tiles fill one round, when the last
+// round is under half full), 2 (default, round 5) the split a
+// list-scheduling model of the launch says ends first (tail_makespan).
+static int tail_split_mode() {
+    static const int v = [] {
         const char *e = getenv("LIFE_TAIL_SPLIT");
-        return e ? atoi(e) != 0 : true;
+        const int m = e ? atoi(e) : 2;
+        return m >= 0 && m <= 2 ? m : 2;
     }();
-    return on;
+    return v;
+}
+// Length in full-tile times of a launch of `full` tiles then `half` tiles of
+// half the duration dealt in order to `slots` resident workgroups, rounds
+// ending together (scripts/tail_model.py): after r = full / slots rounds the
+// rem = full % slots last full tiles hold their slots one more unit while the
+// others take half tiles, two per unit.
+static double tail_makespan(int64_t full, int64_t half, int64_t slots) {
+    const int64_t r = full / slots, rem = full % slots;
+    if (half == 0) return (double)(r + (rem ? 1 : 0));
+    if (rem == 0) return (double)r + 0.5 * (double)((half + slots - 1) / slots);
+    const int64_t gap = 2 * (slots - rem);  // half tiles done in the last full round's idle slots
+    if (half <= gap) return (double)(r + 1);
+    return (double)(r + 1) + 0.5 * (double)((half - gap + slots - 1) / slots);
 }
 
 // resident workgroups of a kernel on this device (occupancy)
@@ -1973,7 +1990,7 @@ hipError_t launch_tstep(const life_layout &Lin, const uint8_t *in, uint8_t *out,
     int64_t items = a.first[a.nreg];  // one workgroup per tile (or banded item)
     a.half_first = a.half_y = a.half_ntx = a.half_yend = 0;
     const int64_t T2 = (int64_t)tile_waves(bit) * (temporal_rows(bit) / 2) - 2 * (int64_t)tile_ghost(L, m);
-    if (bit && T2 >= 1 && a.nreg == 1 && a.tx0[0] == 0 && a.tx1[0] == g.ntx && tail_split_enabled()) {
+    if (bit && T2 >= 1 && a.nreg == 1 && a.tx0[0] == 0 && a.tx1[0] == g.ntx && tail_split_mode() > 0) {
         // one full-width region: the whole shard, or the interior of a row
         // strip (rows [ra, rb) of tiles; the ring runs concurrently)
         // The launch runs items / slots rounds of equal tiles; a last round
@@ -1989,7 +2006,33 @@ hipError_t launch_tstep(const life_layout &Lin, const uint8_t *in, uint8_t *out,
         const int64_t ty0 = a.ty0[0], ty1 = a.ty1[0], yend = std::min(ty1 * g.rows, L.h);
         // (Splitting whatever the last round's fill measured 1-3 % slower,
         // profiles/r04/tail_u.)
-        if (slots > 0 && items > slots && rem != 0 && rem <= slots / 2) {
+        const int mode = tail_split_mode();
+        if (mode == 2 && slots > 0 && items > slots && rem != 0) {
+            // the bottom q tile rows as half tiles, q chosen by the model
+            // (65536^2 at m = 10: 8.5 tile-times against 9.0 for the rule
+            // of mode 1; ties keep more full tiles); q = 0: no split
+            double best = tail_makespan(items, 0, slots);
+            int64_t bq = 0;
+            for (int64_t q = 1; q < ty1 - ty0; ++q) {
+                const int64_t F = ty1 - q;
+                const int64_t full = region_items(g, TileRegion{0, g.ntx, ty0, F});
+                const int64_t half = ((yend - F * g.rows + T2 - 1) / T2) * g.ntx;
+                const double t = tail_makespan(full, half, slots);
+                if (t < best - 1e-9) {
+                    best = t;
+                    bq = q;
+                }
+            }
+            if (bq > 0) {
+                a.ty1[0] = ty1 - bq;
+                a.first[1] = region_items(g, TileRegion{0, g.ntx, ty0, a.ty1[0]});
+                a.half_first = a.first[1];
+                a.half_y = a.ty1[0] * g.rows;
+                a.half_yend = yend;
+                a.half_ntx = g.ntx;
+                items = a.half_first + ((yend - a.half_y + T2 - 1) / T2) * g.ntx;
+            }
+        } else if (mode == 1 && slots > 0 && items > slots && rem != 0 && rem <= slots / 2) {
             int64_t q = 1;
             while (q < ty1 - ty0 && ((q * g.rows + T2 - 1) / T2) * g.ntx < slots) ++q;
             if (q < ty1 - ty0) {

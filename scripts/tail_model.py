@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""List-scheduling model of one bit-tile launch: a pass of
+full tiles (NW x R window rows, T = NW*R - 2m owned) and, for the bottom tile
+rows, half-height tiles (T2 = NW*R/2 - 2m owned, half the duration), dealt in
+order to `slots` resident workgroups.  Prints, per shape, the ideal length
+in tile-times (tiles / slots), no split, the split launch_tstep makes, and
+the best split over every boundary -- the 32768^2 pass is 2.17 ideal, 2.5 at
+best, which is why geometry alone does not fix the small shapes.
+
+    python3 scripts/tail_model.py [slots]
+"""
+import heapq
+import sys
+
+
+def makespan(nfull, nhalf, slots, dh=0.5):
+    free = [0.0] * slots
+    end = 0.0
+    for d, n in ((1.0, nfull), (dh, nhalf)):
+        for _ in range(n):
+            t = heapq.heappop(free) + d
+            end = max(end, t)
+            heapq.heappush(free, t)
+    return end
+
+
+def geom(W, m, R=24, NW=8):
+    T, T2 = NW * R - 2 * m, NW * R // 2 - 2 * m
+    ntx = -(-W // 62)
+    o = W - 62 * (ntx - 1)
+    gsh = 2
+    while (1 << gsh) < o + 2:
+        gsh += 1
+    B = 64 >> gsh if gsh <= 5 else 1  # banded last column: B tile rows per item
+    return T, T2, ntx, B
+
+
+def items(ntx, B, rows):
+    return (ntx - 1) * rows + -(-rows // B) if B > 1 else ntx * rows
+
+
+def current_split(W, h, m, slots):  # life_kernels.hip launch_tstep's rule
+    T, T2, ntx, B = geom(W, m)
+    nty = -(-h // T)
+    n = items(ntx, B, nty)
+    rem = n % slots
+    if n > slots and rem and rem <= slots // 2:
+        q = 1
+        while q < nty and (-(-(q * T) // T2)) * ntx < slots:
+            q += 1
+        F = nty - q
+        return makespan(items(ntx, B, F), -(-(h - F * T) // T2) * ntx, slots)
+    return makespan(n, 0, slots)
+
+
+def main():
+    slots = int(sys.argv[1]) if len(sys.argv) > 1 else 768
+    for name, W, h in [("65536^2", 1024, 65536), ("32768x65536", 512, 65536), ("32768^2", 512, 32768),
+                       ("16384x32768", 256, 32768)]:
+        for m in (10, 12):
+            T, T2, ntx, B = geom(W, m)
+            nty = -(-h // T)
+            n = items(ntx, B, nty)
+            best = min((makespan(items(ntx, B, F), -(-max(h - F * T, 0) // T2) * ntx, slots), F)
+                       for F in range(nty + 1))
+            print(f"{name:12s} m={m:2d} tiles={n:5d} ideal={n / slots:.2f} no-split={makespan(n, 0, slots):.2f} "
+                  f"split={current_split(W, h, m, slots):.2f} best={best[0]:.2f} (full tile rows {best[1]} of {nty})")
+
+
+if __name__ == "__main__":
+    main()
