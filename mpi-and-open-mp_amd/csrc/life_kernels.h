@@ -92,6 +92,11 @@ int flow_slots(const life_layout &L);  // resident workgroups of L's dataflow ke
 int tile_slots(const life_layout &L);  // resident workgroups of L's per-launch tile kernel on this device
 // ev0 / ev1 (optional): events stamped with the kernel dispatch's own start
 // and end (hipExtLaunchKernel) -- no event packets between launches.
+// One empty launch of the dataflow instance launch_tflow(L, m, flow) would use
+// (and its occupancy query): the first launch of a kernel in a process costs
+// ~140 us, which a device pays here at creation instead of inside its first
+// dataflow step call.  `head`: the caller's scratch (2 words).
+hipError_t prewarm_tflow(const life_layout &L, int m, int flow, unsigned int *head, hipStream_t s);
 hipError_t launch_tflow(const life_layout &L, const uint8_t *in, uint8_t *out, int m, int64_t passes,
                         unsigned int *head, unsigned int *done, Wrap wrap, int flow, hipStream_t s,
                         hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);

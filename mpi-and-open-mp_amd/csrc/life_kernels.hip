@@ -2117,6 +2117,17 @@ int flow_slots(const life_layout &L) {
     return cached;
 }
 
+hipError_t prewarm_tflow(const life_layout &L, int m, int flow, unsigned int *head, hipStream_t s) {
+    const TileGeom g = tile_geom(L, m);
+    const void *fn = flow_kernel_of(L, flow, flow_band(g));
+    if (!fn || !flow_ok(L, m) || flow_slots(L) <= 0) return hipErrorInvalidValue;  // (caches the slot count)
+    FArgs f{};  // no items: the one workgroup pulls item 0 and leaves
+    f.head = head;
+    const hipError_t e = hipMemsetAsync(head, 0, sizeof(unsigned int), s);
+    if (e != hipSuccess) return e;
+    return launch_fn(fn, 1u, 64u * (unsigned)tile_waves(true), &f, s, nullptr, nullptr);
+}
+
 hipError_t launch_tflow(const life_layout &L, const uint8_t *in, uint8_t *out, int m, int64_t passes,
                         unsigned int *head, unsigned int *done, Wrap wrap, int flow, hipStream_t s, hipEvent_t ev0,
                         hipEvent_t ev1) {
