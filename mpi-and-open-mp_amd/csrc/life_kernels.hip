@@ -353,12 +353,6 @@ struct XchB {
 // read beyond the tile, absorbed by the ghost lanes.  Only the loads and
 // stores differ (per-lane rows); the generation loop is the tile's.  gsh = 6:
 // an ordinary tile (nb = 1).
-// LIFE_FLOW_EXP (timing-only diagnostics builds, results may be stale; never
-// in the product build): bit 1 plain window loads in the dataflow tiles, 2
-// plain stores, 4 no store drain before the hand-off flag.
-#ifndef LIFE_FLOW_EXP
-#define LIFE_FLOW_EXP 0
-#endif
 // LIFE_FLOW_BP_AHEAD (default 1): the dataflow tiles' generation loop issues
 // each row's two neighbour permutes that many rows ahead of their use, rows
 // fenced in program order.  Left to itself the compiler scheduled that loop
@@ -433,7 +427,7 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             uint64_t q;
-            if (FLOW && !(LIFE_FLOW_EXP & 1))
+            if (FLOW)
                 q = __hip_atomic_load(reinterpret_cast<uint64_t *>(const_cast<uint8_t *>(p) + voff),
                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             else
@@ -566,7 +560,7 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
         if (r < r0 || r >= r1) continue;
         if (st && yb + r < ylim) {
             const uint64_t v = (uint64_t)ve[r] | ((uint64_t)vo[r] << 32);
-            if (FLOW == 1 && !(LIFE_FLOW_EXP & 2))
+            if (FLOW == 1)
                 __hip_atomic_store(reinterpret_cast<uint64_t *>(q), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             else
                 *reinterpret_cast<uint64_t *>(q) = v;
@@ -948,7 +942,7 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tflow_kernel(FArgs f)
             tile_body_bit<R, WRAPX, WRAPY, FLOW, NW, true>(a, in, out, tx, ty, xch, a.gsh, nb);
         else
             tile_body_bit<R, WRAPX, WRAPY, FLOW, NW>(a, in, out, tx, ty, xch);
-        if (!(LIFE_FLOW_EXP & 4)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
         __syncthreads();
         if (LIFE_WG_TRACE && traced < 4) wg_trace(3 + 3 * traced++);
         prev_flag = f.done + ty * f.ntx + tx;
