@@ -40,8 +40,9 @@ VARIANTS = {  # variant -> (kernel-name substrings (any round's name), calibrate
     "bit_flow": (("tflow_kernel<",), True),  # sc1; one dispatch = PASSES[var] passes
 }
 # dataflow launches run several passes per dispatch: the PMC job times a
-# 80-generation call at 20 generations per pass (profiles/r02/jobs/r2r.sh)
-PASSES = {"bit_flow": 4}
+# 80-generation call at 20 generations per pass (profiles/r02/jobs/r2r.sh);
+# FLOW_PASSES overrides (profiles/r05/z: a 96-generation call, 8 x 12)
+PASSES = {"bit_flow": int(os.environ.get("FLOW_PASSES", "4"))}
 
 out = {}
 for var, (needle, calibrated) in VARIANTS.items():
