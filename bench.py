@@ -29,8 +29,12 @@ max-over-ranks timing; the halo data path is RCCL ncclSend/ncclRecv issued by
 liblife_mi355x.so itself.  `--gpus N` without a launcher and with N GPUs
 visible spawns those N rank processes itself (spawn_ranks) before any HIP
 call; `--single-process` instead drives the N GPUs from one process
-(ncclCommInitAll), and with fewer GPUs than shards one process runs them with
-device-local copies (how a 1-GPU box rehearses the partitioned schedule).
+(ncclCommInitAll).  With fewer visible GPUs than --gpus the run is refused
+unless --rehearse-shards is given: then one process runs the N shards with
+device-local copies (how a 1-GPU box rehearses the partitioned schedule) and
+the line says n_gpus = the devices actually used, config.shards = N.  Every
+line carries config.devices (distinct PCI bus ids over all ranks) and
+config.rccl_nranks (ncclCommCount).
 `--shape WxH` replaces --size^2 (the per-GPU blocks of configs[3]).
 Every N > 1 line ends with "phases" (mean ring / interior / halo / block
 times per exchange, from HIP events on the three streams) and
@@ -103,6 +107,10 @@ def parse():
     p.add_argument("--single-process", action="store_true",
                    help="--gpus N > 1 without a launcher: drive the N GPUs from this one process "
                         "(ncclCommInitAll) instead of spawning one process per GPU")
+    p.add_argument("--rehearse-shards", action="store_true",
+                   help="allow --gpus N above the visible GPU count: one process drives the N shards on the GPUs "
+                        "there are (LOCAL device copies); the line then reports n_gpus = the devices actually used "
+                        "and config.shards = N.  Without it such a run is refused")
     p.add_argument("--loopback", action="store_true",
                    help="N = 1: run the single grid as a periodic partition of itself (LIFE_OPT_LOOPBACK): the "
                         "halo exchange, ring / interior overlap and (with --rank-mode) RCCL send/recv of the "
@@ -163,6 +171,27 @@ def make_life(a, nx, ny, dims, rank_mode, dist, rank, world, local_rank):
     if a.no_overlap:
         life.configure(lm.OPT_OVERLAP, 0)
     return life
+
+
+def topology(life, dist, world):
+    """What the run actually used: the distinct physical
+    GPUs (PCI bus ids) over every shard of every rank, and the rank count of
+    the RCCL communicators (ncclCommCount; 0 = no communicator, LOCAL
+    copies).  Collective in rank mode (gloo all_gather_object)."""
+    infos = [life.shard_info(i) for i in range(life.world()["nlocal"])]
+    if any(x is None for x in infos):
+        return None
+    buses = [x["pci_bus_id"] for x in infos]
+    nranks = [x["rccl_nranks"] for x in infos]
+    if dist is not None and world > 1:
+        allb, alln = [None] * world, [None] * world
+        dist.all_gather_object(allb, buses)
+        dist.all_gather_object(alln, nranks)
+        buses = [b for part in allb for b in part]
+        nranks = [n for part in alln for n in part]
+    lo, hi = min(nranks), max(nranks)
+    return {"devices": len(set(buses)), "pci_bus_ids": sorted(set(buses)),
+            "rccl_nranks": lo if lo == hi else [lo, hi]}
 
 
 def init_grid(life, a, grid):
@@ -274,10 +303,17 @@ def spawn_ranks(n: int, argv, child=None) -> int:
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world == 1 and "RANK" not in os.environ and a.gpus > 1 and not a.single_process and not a.rank_mode:
-        if visible_gpus() >= a.gpus:
+    if world == 1 and "RANK" not in os.environ and a.gpus > 1 and not a.rank_mode:
+        # no line may claim N GPUs it did not run on
+        visible = visible_gpus()
+        if visible >= a.gpus and not a.single_process:
             child = os.environ.get("LIFE_BENCH_CHILD_CMD")  # tests: a stand-in for the rank processes
             sys.exit(spawn_ranks(a.gpus, sys.argv[1:], json.loads(child) if child else None))
+        if visible < a.gpus and not a.rehearse_shards:
+            print(f"bench.py: --gpus {a.gpus} but {visible} GPU(s) visible; refusing to report an {a.gpus}-GPU line "
+                  f"from fewer devices (pass --rehearse-shards to run {a.gpus} shards on the GPUs there are)",
+                  file=sys.stderr, flush=True)
+            sys.exit(2)
     lm._lib()
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -323,6 +359,7 @@ def main():
         workload = f"random 50% {shape_txt} per GPU, global {nx}x{ny} ({label})"
 
     life = make_life(a, nx, ny, dims, rank_mode, dist, rank, world, local_rank)
+    topo = topology(life, dist, world)
     init_grid(life, a, grid)
     if a.loopback:
         if n_gpus != 1:
@@ -414,6 +451,10 @@ def main():
         if path == "flow" and a.kernel == "bit":
             variant = "bit_flow"
         traffic = load_traffic(variant, shape_txt.replace("^2", "")) if (a.workload == "random" and not strong) else None
+        # not measured by this run: the PMC pass of the same workload committed beside the code
+        traffic_src = (f"profiles/traffic.json[{variant}_{shape_txt.replace('^2', '')}] (committed rocprofv3 "
+                       "FETCH_SIZE x2 + WRITE_SIZE run of this workload, bytes per launch; not this run)"
+                       if traffic is not None else None)
         hbm_obj = {"achieved": round(hbm, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                    "frac": round(hbm / HBM_PEAK_GBS, 4),
                    "bytes_per_launch": bytes_per_launch,
@@ -443,6 +484,7 @@ def main():
             useful = algo / (avg_ms * 1e-3) / 1e12
             roofline = {"bound": "valu", "achieved": round(useful, 2), "peak": round(VALU_PEAK_TOPS, 2),
                         "unit": "Tlane-op/s", "frac": round(useful / VALU_PEAK_TOPS, 4), "traffic": traffic,
+                        "traffic_source": traffic_src,
                         "kernel_avg_ms": round(avg_ms, 5), "kernel_launches": launches,
                         "kernel_timing": ("HIP events on the launches of K generations after the timed call "
                                           "(a multi-stream call is timed by its span only)") if stats_after
@@ -457,13 +499,15 @@ def main():
                                  "life_kernels.hip tile_body_bit / tile_body_byte",
                         "hbm": hbm_obj}
         else:
-            roofline = dict(hbm_obj, bound="hbm", traffic=traffic, kernel_avg_ms=round(avg_ms, 5),
+            roofline = dict(hbm_obj, bound="hbm", traffic=traffic, traffic_source=traffic_src, kernel_avg_ms=round(avg_ms, 5),
                             kernel_launches=launches, generations_per_launch=round(gens_per_launch, 3))
         out = {
             "metric": "Gcell-updates/sec at 1/2/4/8 MI355X + % of HBM roofline, bit-exact",
             "value": round(value, 3),
             "unit": "Gcell-updates/s",
-            "n_gpus": n_gpus,
+            # the distinct GPUs the shards ran on (a --rehearse-shards run of
+            # N shards on one GPU says 1 here and shards = N in config)
+            "n_gpus": topo["devices"] if topo else n_gpus,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 4),
@@ -474,6 +518,10 @@ def main():
             "data": "synthetic (device-side splitmix64 random, density 0.5)" if grid is None
                     else "p46gun_big.cfg pattern",
             "config": {"workload": workload, "nx": nx, "ny": ny, "dims": list(dims), "kernel": a.kernel,
+                       "shards": n_gpus, "devices": topo["devices"] if topo else None,
+                       "rccl_nranks": topo["rccl_nranks"] if topo else None,
+                       "pci_bus_ids": topo["pci_bus_ids"] if topo else None,
+                       "rehearsal": bool(topo and topo["devices"] < n_gpus),
                        "parallelism": f"cartesian {dims[0]}x{dims[1]}"
                                       + (" (one process per GPU, RCCL)" if rank_mode else
                                          f" ({life.world()['nlocal']} shards in one process, "

@@ -138,6 +138,7 @@ int life_layout_query(int64_t nx, int64_t ny, int dims0, int dims1, int rank, in
                       life_layout *out);
 
 const char *life_strerror(int err);
+const char *life_dev_strerror(int err); /* the same (SURVEY 8(b)'s name for it) */
 const char *life_last_error(void); /* detail of the last LIFE_EHIP/ERCCL on this thread */
 
 /* ---------------------------------------------------------------- device */
@@ -219,6 +220,12 @@ int life_dev_barrier(life_dev *d);
 int life_device_count(void);
 int life_dev_layout(life_dev *d, int local_shard, life_layout *out);
 int life_dev_world(life_dev *d, int *world, int *dims0, int *dims1, int *nlocal, int *transport);
+/* Where local shard `local_shard` runs (measurement support, so a multi-GPU
+ * result can prove what it ran on): its HIP device ordinal, that device's PCI
+ * bus id (hipDeviceGetPCIBusId; distinct per physical GPU, up to 63 chars +
+ * NUL), and the rank count of its RCCL communicator (ncclCommCount; 0 when
+ * the shard has none, e.g. LOCAL transport).  Any out pointer may be NULL. */
+int life_dev_shard_info(life_dev *d, int local_shard, int *device, char pci_bus_id[64], int *rccl_nranks);
 
 /* Kernel timing for roofline reporting: when on, every stencil launch is
  * bracketed by HIP events on the stream it runs on.  stats returns the mean
@@ -297,9 +304,14 @@ int life_dev_set_timing(life_dev *d, int on);
  * the apron cells they will read (rows [-e, 0) and [h, h + e), the apron
  * pairs), so one exchange feeds up to K generations instead of one pass of
  * at most LIFE_OPT_BLOCK_GENS.  0: one exchange per pass.  Same results.
- * Setting it communicates nothing (not a collective; ranks may differ):
- * part-used aprons are refilled by the next step's first pass that needs
- * them.  Every life_dev_configure call waits for the device (life_dev_sync). */
+ * The value decides which passes exchange, so every rank must hold the same
+ * one: in rank mode (world > 1) this option is COLLECTIVE -- every rank calls
+ * it with the same value at the same step boundary; it checks agreement
+ * with an RCCL all-reduce and fails with LIFE_EINVAL (all ranks keep the old
+ * value) when ranks differ, or with LIFE_ERCCL after LIFE_COMM_TIMEOUT_S when
+ * a rank never calls it.  Part-used aprons are refilled by the next step's
+ * first pass that needs them.  Every life_dev_configure call waits for the
+ * device (life_dev_sync). */
 #define LIFE_OPT_DEEP_HALO 9
 /* Option 10 (LIFE_OPT_SKEW, time-skewed ghost-free tiles) was retired in
  * round 5: 8 % slower per launch on MI355X; it now fails

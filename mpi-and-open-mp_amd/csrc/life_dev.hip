@@ -541,7 +541,7 @@ int launch_region(life_dev *d, Shard &s, const life::Region &r, bool timed, hipS
         if (ev) HIPCHK(hipEventRecord(t->a, st));
     }
     HIPCHK(life::launch_step(s.lay, in, out, s.sink, r, wrap_of(d), st));
-    if (d->timing && timed && t) {  // (span-only timing books no launches)
+    if (d->timing && timed && t) {  // (no timer counts it -- span-only timing, LIFE_TIMING_MODE=3: no booking)
         if (ev) HIPCHK(hipEventRecord(t->b, st));
         const bool bit = s.lay.kernel == LIFE_KERNEL_BIT;
         const int64_t cpu = bit ? 128 : 16;
@@ -626,7 +626,7 @@ int launch_tiles(life_dev *d, Shard &s, const life::TileRegion *r, int nreg, int
     HIPCHK(life::launch_tstep(s.lay, in, out, r, nreg, m, wrap_of(d), st, &valu, ext ? t->a : nullptr,
                               ext ? t->b : nullptr, xt));
     if (ev && !ext) HIPCHK(hipEventRecord(t->b, st));
-    if (d->timing && timed && t) {  // (span-only timing books no launches)
+    if (d->timing && timed && t) {  // (no timer counts it -- span-only timing, LIFE_TIMING_MODE=3: no booking)
         const life::TileGeom g = life::tile_geom(life::extended_layout(s.lay, xt), m);
         for (int k = 0; k < nreg; k++) {
             // owned cells only (a deep-halo pass's apron rows are not counted)
@@ -867,6 +867,13 @@ int generation(life_dev *d) {
     for (size_t si = 0; si < d->shards.size(); ++si) {
         Shard &s = d->shards[si];
         HIPCHK(hipSetDevice(s.device));
+        // The interior (second stream) starts after everything on the compute
+        // stream: phase_end joined the previous generation into ONE stream
+        // only (and may have swapped the handles), so without this fence the
+        // next interior could start beside the previous interior (still
+        // reading cur) or beside the previous ring + halo.
+        HIPCHK(hipEventRecord(s.ev_entry, s.stream));
+        HIPCHK(hipStreamWaitEvent(s.stream2, s.ev_entry, 0));
         CHK(phase_begin(d, s, &pe[si]));
         const int64_t U = s.lay.units, H = s.lay.h;
         const int64_t ra = ry ? 1 : 0, rb = ry ? H - 1 : H;  // interior rows
@@ -931,6 +938,28 @@ int bounded_sync(Shard &s, const char *what, int peer, hipStream_t st = nullptr)
         // as wait_stream), then back off to 1 ms naps
         if (dt > 0.02) std::this_thread::sleep_for(std::chrono::microseconds(1000));
     }
+}
+
+// Rank mode: a collective check that every rank passes the same `value`
+// (an int64 max all-reduce of {value, -value}); bounded like the barrier.
+int agree_all_ranks(life_dev *d, int value, const char *what) {
+    for (Shard &s : d->shards) {
+        if (!s.comm) continue;
+        HIPCHK(hipSetDevice(s.device));
+        int64_t *h = reinterpret_cast<int64_t *>(s.h_count);
+        h[0] = value;
+        h[1] = -(int64_t)value;
+        HIPCHK(hipMemcpyAsync(s.d_count, h, 2 * sizeof(int64_t), hipMemcpyHostToDevice, s.stream));
+        NCCLCHK(ncclAllReduce(s.d_count, s.d_count, 2, ncclInt64, ncclMax, s.comm, s.stream));
+        HIPCHK(hipMemcpyAsync(h, s.d_count, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, s.stream));
+        CHK(bounded_sync(s, what, -1));
+        const int64_t hi = h[0], lo = -h[1];
+        if (hi != lo) {
+            set_err("%s is collective in rank mode: ranks passed %lld .. %lld", what, (long long)lo, (long long)hi);
+            return LIFE_EINVAL;
+        }
+    }
+    return LIFE_OK;
 }
 
 int create_common(life_dev *d, const std::vector<int> &ranks, const std::vector<int> &devices) {
@@ -1275,7 +1304,10 @@ static int step_flow(life_dev *d, int64_t generations, int64_t *done) {
         HIPCHK(life::launch_tflow(L, s.buf[s.cur], s.buf[s.cur ^ 1], m, n, s.flow, s.flow + 2, wrap_of(d),
                                   form, s.stream, ext ? t->a : nullptr, ext ? t->b : nullptr));
         if (ev && !ext) HIPCHK(hipEventRecord(t->b, s.stream));
-        if (d->timing) {
+        // work is booked only beside a timer that counts the launch (as
+        // launch_tiles / launch_region: LIFE_TIMING_MODE=3 and span-only
+        // timing book nothing, so bytes / updates per launch stay consistent)
+        if (d->timing && t) {
             const double cells = (double)L.w * (double)L.h;
             d->acc_bytes += (double)n * cells * 0.25;
             d->acc_updates += (double)n * cells * (double)m;
@@ -1689,6 +1721,19 @@ int life_dev_world(life_dev *d, int *world, int *dims0, int *dims1, int *nlocal,
     return LIFE_OK;
 }
 
+int life_dev_shard_info(life_dev *d, int local_shard, int *device, char pci_bus_id[64], int *rccl_nranks) {
+    if (!d || local_shard < 0 || local_shard >= (int)d->shards.size()) return LIFE_EINVAL;
+    const Shard &s = d->shards[local_shard];
+    if (device) *device = s.device;
+    if (pci_bus_id) HIPCHK(hipDeviceGetPCIBusId(pci_bus_id, 64, s.device));
+    if (rccl_nranks) {
+        int n = 0;
+        if (s.comm) NCCLCHK(ncclCommCount(s.comm, &n));
+        *rccl_nranks = n;
+    }
+    return LIFE_OK;
+}
+
 int life_dev_configure(life_dev *d, int option, int value) {
     if (!d) return LIFE_EINVAL;
     CHK(life_dev_sync(d));
@@ -1721,9 +1766,12 @@ int life_dev_configure(life_dev *d, int option, int value) {
         return LIFE_OK;
     case LIFE_OPT_DEEP_HALO:
         if (value < 0 || value > 1) return LIFE_EINVAL;
-        // no communication here: aprons valid only to the
-        // remaining depth K - since are refilled by the next pass that needs
-        // more (generation_block), so the option is local to each rank
+        // Aprons valid only to the remaining depth K - since are refilled by
+        // the next pass that needs more (generation_block).  But the option
+        // decides which passes exchange, so in rank mode every rank must hold
+        // the same value or their ncclSend / ncclRecv groups stop pairing up
+        // (ADVICE r5): the call is collective there and checks agreement.
+        if (d->rank_mode && d->world > 1) CHK(agree_all_ranks(d, value, "LIFE_OPT_DEEP_HALO"));
         d->deep = value != 0;
         return LIFE_OK;
     case LIFE_OPT_FLOW_CHUNK:

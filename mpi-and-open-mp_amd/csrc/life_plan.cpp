@@ -286,4 +286,7 @@ const char *life_strerror(int err) {
     }
 }
 
+// SURVEY 8(b)'s proposed name for the same function
+const char *life_dev_strerror(int err) { return life_strerror(err); }
+
 }  // extern "C"

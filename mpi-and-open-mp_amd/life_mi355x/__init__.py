@@ -61,6 +61,7 @@ ABI_SYMBOLS = (
     "life_tune", "life_tune_temporal", "life_dev_configure", "life_dev_kernel_work", "life_dev_checksum",
     "life_dev_gather_vtk", "life_dev_gather_bits", "life_dev_destroy", "life_measure_copy", "life_dev_phase_stats",
     "life_dev_barrier", "life_device_count", "life_dev_last_path", "life_dev_call_stats",
+    "life_dev_strerror", "life_dev_shard_info",
 )
 PATHS = {0: "none", 1: "onegen", 2: "tiles", 3: "flow", 5: "small"}
 
@@ -157,6 +158,8 @@ def _lib():
         L.life_dev_phase_stats.argtypes = [vp] + [P(ctypes.c_double)] * 4 + [P(i64)]
         if hasattr(L, "life_dev_call_stats"):  # absent from pre-round-4 builds (LIFE_MI355X_LIB A/B runs)
             L.life_dev_call_stats.argtypes = [vp, P(ctypes.c_double), P(ctypes.c_double), P(i64), P(ctypes.c_double)]
+        if hasattr(L, "life_dev_shard_info"):  # absent from pre-round-6 builds (LIFE_MI355X_LIB A/B runs)
+            L.life_dev_shard_info.argtypes = [vp, i32, P(ctypes.c_int), ctypes.c_char_p, P(ctypes.c_int)]
         L.life_tune.argtypes = [i32, i32, i32]
         L.life_tune_temporal.argtypes = [i32, i32]
         L.life_measure_copy.argtypes = [i32, i64, i32, P(ctypes.c_double)]
@@ -373,6 +376,18 @@ class Life:
         v = [ctypes.c_int() for _ in range(5)]
         _check(_lib().life_dev_world(self._h, *[ctypes.byref(x) for x in v]), "world")
         return dict(zip(("world", "dims0", "dims1", "nlocal", "transport"), (x.value for x in v)))
+
+    def shard_info(self, local_shard: int = 0):
+        """life_dev_shard_info: {"device", "pci_bus_id", "rccl_nranks"} of a
+        local shard (rccl_nranks 0: no communicator); None from builds that
+        predate it."""
+        if not hasattr(_lib(), "life_dev_shard_info"):
+            return None
+        dev, n = ctypes.c_int(), ctypes.c_int()
+        bus = ctypes.create_string_buffer(64)
+        _check(_lib().life_dev_shard_info(self._h, local_shard, ctypes.byref(dev), bus, ctypes.byref(n)),
+               "shard_info")
+        return {"device": dev.value, "pci_bus_id": bus.value.decode(errors="replace"), "rccl_nranks": n.value}
 
     def set_timing(self, on) -> None:
         """life_dev_set_timing: False off, True launch timing + phase events,

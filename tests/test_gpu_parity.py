@@ -68,6 +68,26 @@ def test_multi_shard_local(gpu, oracle, kernel, shards, dims, nx, ny, overlap):
         assert life.live_count() == int(want.sum())
 
 
+@pytest.mark.parametrize("kernel", ["byte", "bit"])
+def test_onegen_wide_interior_local(gpu, oracle, kernel):
+    """the overlapped one-generation schedule joins each
+    generation into ONE stream, so the next interior must be fenced behind
+    everything on the compute stream.  Row strips 24 rows tall (< K: the
+    one-generation layout) and 131072 cells wide: each shard's interior (22
+    rows) runs far longer than its ring (2 rows) + halo, the shape where a
+    missing fence lets two generations' interiors overlap."""
+    nx, ny, shards = 131072, 16 * 24, 16
+    g0 = oracle.fill_random(nx, ny, seed=5, density=0.5)
+    with gpu.Life(nx, ny, shards=shards, kernel=kernel, dims=(1, shards), transport=gpu.XPORT_LOCAL) as life:
+        assert life.layout().generations_per_exchange == 1
+        life.upload(g0)
+        life.step(1)
+        np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, 1, threads=8), err_msg="generation 1")
+        life.step(9)
+        assert life.last_path() == "onegen"
+        np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, 10, threads=8), err_msg="generation 10")
+
+
 @pytest.mark.parametrize("nx", [1024, 1000], ids=["temporal", "onegen"])
 def test_byte_equals_bit_long(gpu, oracle, nx):
     ny, gens = 768, 200
@@ -446,3 +466,36 @@ def test_deep_halo_exchange_count(gpu, oracle, rccl):
 
 
 
+
+
+_TIMING_OFF = r"""
+import sys
+sys.path.insert(0, {pkg!r})
+import life_mi355x as lm
+for flow in (0, 1):
+    with lm.Life(4096, 4096, kernel="bit", small_grid=False, flow=flow) as life:
+        life.fill_random(1)
+        life.set_timing(True)
+        life.step(72)
+        path = life.last_path()
+        assert path == ("flow" if flow else "tiles"), path
+        ms, n, b = life.kernel_stats()
+        upd, valu = life.kernel_work()
+        assert (n, b, upd, valu) == (0, 0.0, 0.0, 0.0), (path, n, b, upd, valu)
+print("TIMING_OFF_OK", flush=True)
+"""
+
+
+def test_timing_mode_off_books_nothing(gpu):
+    """under LIFE_TIMING_MODE=3 no launch is timed, so no
+    work may be booked either -- the tiles and the dataflow passes alike --
+    or bytes / updates per launch come out of a count of zero launches."""
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+
+    env = dict(os.environ, LIFE_TIMING_MODE="3")
+    out = subprocess.run([sys.executable, "-c", _TIMING_OFF.format(pkg=os.path.join(ROOT, "mpi-and-open-mp_amd"))],
+                         env=env, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0 and "TIMING_OFF_OK" in out.stdout, out.stdout + out.stderr
