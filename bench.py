@@ -111,6 +111,9 @@ def parse():
                    help="allow --gpus N above the visible GPU count: one process drives the N shards on the GPUs "
                         "there are (LOCAL device copies); the line then reports n_gpus = the devices actually used "
                         "and config.shards = N.  Without it such a run is refused")
+    p.add_argument("--loopback-axes", default="xy", choices=["xy", "x", "y"],
+                   help="--loopback: the axes exchanged through the transport (x: columns only, as N = 2's {2,1} "
+                        "blocks; the other axis wraps in the stencil)")
     p.add_argument("--loopback", action="store_true",
                    help="N = 1: run the single grid as a periodic partition of itself (LIFE_OPT_LOOPBACK): the "
                         "halo exchange, ring / interior overlap and (with --rank-mode) RCCL send/recv of the "
@@ -364,7 +367,7 @@ def main():
     if a.loopback:
         if n_gpus != 1:
             raise SystemExit("--loopback is a one-GPU mode")
-        life.configure(lm.OPT_LOOPBACK, 1)
+        life.configure(lm.OPT_LOOPBACK, {"xy": 1, "x": 2, "y": 3}[a.loopback_axes])
     # The timed call of a single-stream step (one shard, no partitioned
     # axis: the N = 1 lines) carries one event pair around all its launches
     # (set_timing(2) keeps it so).  A multi-stream step (N > 1, --loopback)
@@ -526,7 +529,8 @@ def main():
                                       + (" (one process per GPU, RCCL)" if rank_mode else
                                          f" ({life.world()['nlocal']} shards in one process, "
                                          f"{['auto', 'RCCL', 'LOCAL'][life.world()['transport']]} transport)"),
-                       "partition": partition + (" + loopback (the shard its own neighbour)" if a.loopback else ""), "kernel_path": path,
+                       "partition": partition + (f" + loopback of axes {a.loopback_axes} (the shard its own neighbour)"
+                                                 if a.loopback else ""), "kernel_path": path,
                        "generations_per_exchange": lay.generations_per_exchange, "live_cells_end": live},
             "roofline": roofline,
             # the timed call, self-diagnosing: CPU time

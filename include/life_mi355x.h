@@ -278,7 +278,9 @@ int life_dev_set_timing(life_dev *d, int on);
  * (life_dev_create_rank, world 1, a unique id) the messages are RCCL
  * ncclSend/ncclRecv: how one GPU executes the multi-GPU data path.  Results
  * are identical either way.  The grid must be at least one halo deep
- * (generations_per_exchange rows). */
+ * (generations_per_exchange rows).  Value 2 loops the x axis only, 3 the y
+ * axis only (the other axis wraps in the stencil): the axes a real partition
+ * cuts -- N = 2's {2, 1} blocks exchange columns only. */
 #define LIFE_OPT_LOOPBACK 6
 /* LIFE_OPT_FLOW (default 3, automatic, or LIFE_FLOW from the environment): a step call
  * on a single shard whose axes both wrap inside it (bit encoding, width a

@@ -203,7 +203,7 @@ struct life_dev {
     int small_mode = 1;  // grids that fit one CU: 0 off, 1 VGPR kernel else LDS kernel, 2 LDS kernel,
                         // 3 windowed VGPR kernel over several CUs (else as 1), 4 as 1 never windowed
     int win_rows = 0, win_halo = 0;  // windowed kernel: strip height R, halo rows K (0: automatic)
-    bool loop = false;  // LIFE_OPT_LOOPBACK: the one shard exchanges both axes' halos with itself
+    int loop = 0;  // LIFE_OPT_LOOPBACK: axes (bit 0 x, bit 1 y) whose halos the one shard exchanges with itself
     int last_path = LIFE_PATH_NONE;  // life_dev_last_path
     bool deep = kEnvDeepHalo;  // LIFE_OPT_DEEP_HALO: one K-deep exchange feeds several passes
     int since = 0;  // generations advanced since the aprons were last filled (deep halo)
@@ -231,9 +231,9 @@ namespace {
 
 // Axis a's apron is filled by a halo exchange (dims[a] > 1, or the loopback
 // test mode, where the single shard is its own neighbour on both axes).
-bool part(const life_dev *d, int a) { return d->dims[a] > 1 || d->loop; }
+bool part(const life_dev *d, int a) { return d->dims[a] > 1 || ((d->loop >> a) & 1); }
 // The shard wraps x itself (the x-apron is filled by launch_wrap_columns).
-bool self_wrap_x(const life_dev *d) { return !d->loop && life::self_wrap_x(d->shards[0].lay, d->dims[0]); }
+bool self_wrap_x(const life_dev *d) { return !(d->loop & 1) && life::self_wrap_x(d->shards[0].lay, d->dims[0]); }
 life::Wrap wrap_of(const life_dev *d) { return life::Wrap{!part(d, 0) && !self_wrap_x(d), !part(d, 1)}; }
 
 // Allocation fill of every shard buffer (LIFE_POISON, read at each
@@ -1166,7 +1166,7 @@ static life::RegWinPlan win_plan(const life_dev *d) {
 }
 
 static bool small_grid(const life_dev *d) {
-    if (d->world != 1 || d->shards.size() != 1 || d->small_mode == 0 || d->loop) return false;
+    if (d->world != 1 || d->shards.size() != 1 || d->small_mode == 0 || d->loop != 0) return false;
     const life_layout &L = d->shards[0].lay;
     if (win_plan(d).blocks > 0) return true;
     return (d->small_mode != 2 && life::reg_small_rows(L) > 0) ||
@@ -1779,7 +1779,9 @@ int life_dev_configure(life_dev *d, int option, int value) {
         d->flow_chunk = value;
         return LIFE_OK;
     case LIFE_OPT_LOOPBACK: {
-        if (value < 0 || value > 1) return LIFE_EINVAL;
+        // 1: both axes, 2: x only, 3: y only (the axes a real partition of
+        // N GPUs cuts: N = 2's {2, 1} cuts x only)
+        if (value < 0 || value > 3) return LIFE_EINVAL;
         if (d->world != 1 || d->shards.size() != 1) {
             set_err("loopback needs a single-shard world (world %d, %zu local shards)", d->world, d->shards.size());
             return LIFE_EINVAL;
@@ -1799,7 +1801,7 @@ int life_dev_configure(life_dev *d, int option, int value) {
         }
         // the current state's aprons are refreshed on the next step's first
         // exchange only: fill them now from the shard itself
-        d->loop = value != 0;
+        d->loop = value == 0 ? 0 : value == 1 ? 3 : value == 2 ? 1 : 2;
         life_halo_op ops[16];
         const int n = life::halo_plan(d->nx, d->ny, d->dims[0], d->dims[1], s.rank, d->kernel, d->loop, ops, 16);
         if (n < 0) return LIFE_EINVAL;

@@ -8,9 +8,9 @@
 
 namespace life {
 
-// life_halo_plan with `loop`: an axis with dims == 1 is exchanged too, the
-// shard being its own neighbour (LIFE_OPT_LOOPBACK).
-int halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int kernel, bool loop, life_halo_op *ops,
+// life_halo_plan with `loop` (bit 0: x, bit 1: y): that axis, with dims == 1,
+// is exchanged too, the shard being its own neighbour (LIFE_OPT_LOOPBACK).
+int halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int kernel, int loop, life_halo_op *ops,
               int max_ops);
 
 // The dataflow queue head is 32-bit: one launch may hold at most

@@ -175,10 +175,11 @@ int life::gather_plan(int64_t nx, int64_t ny, int dims0, int dims1, int kernel, 
     return world;
 }
 
-// The halo plan; `loop` treats an axis the shard spans whole (dims == 1) as
-// partitioned too, with the shard as its own left and right neighbour
-// (LIFE_OPT_LOOPBACK: the transport's send/recv path exercised by one rank).
-int life::halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int kernel, bool loop,
+// The halo plan; `loop` (bit 0: x, bit 1: y) treats that axis, which the
+// shard spans whole (dims == 1), as partitioned too, with the shard as its own
+// left and right neighbour (LIFE_OPT_LOOPBACK: the transport's send/recv path
+// exercised by one rank).
+int life::halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int kernel, int loop,
                     life_halo_op *ops, int max_ops) {
     life_layout L;
     const int rc = life_layout_query(nx, ny, dims0, dims1, rank, kernel, &L);
@@ -199,7 +200,7 @@ int life::halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int 
         o.first = first;
         o.count = count;
     };
-    const bool px = dims0 > 1 || loop, py = dims1 > 1 || loop;
+    const bool px = dims0 > 1 || (loop & 1), py = dims1 > 1 || (loop & 2);
     // Both axes exchanged by messages with K-deep temporal aprons: ONE phase
     // (one RCCL group per exchange instead of two back to back, round 5):
     // columns, whole padded rows (their x-apron bytes are stale and are
@@ -214,7 +215,7 @@ int life::halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int 
     // self-messages of one group in 39 us, longer than the two groups of the
     // column and row phases (19 + 14 us; 16384 x 32768, profiles/r05/g),
     // while distinct peers over xGMI are served by separate channels.
-    const bool fused = px && py && L.generations_per_exchange > 1 && !loop;
+    const bool fused = px && py && L.generations_per_exchange > 1 && loop == 0;
     const int ph_rows = fused ? 0 : 1;
     // Phase 0: columns (dim 0 splits x), owned rows only.  MPI_Cart_shift(dim 0).
     if (!px) {
@@ -270,7 +271,7 @@ extern "C" {
 
 int life_halo_plan(int64_t nx, int64_t ny, int dims0, int dims1, int rank, int kernel,
                    life_halo_op *ops, int max_ops) {
-    return life::halo_plan(nx, ny, dims0, dims1, rank, kernel, false, ops, max_ops);
+    return life::halo_plan(nx, ny, dims0, dims1, rank, kernel, 0, ops, max_ops);
 }
 
 const char *life_strerror(int err) {

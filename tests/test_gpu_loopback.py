@@ -150,3 +150,22 @@ def test_loopback_initall_gather_and_frames(gpu, oracle, kernel):
         np.testing.assert_array_equal(life.gather(), want)
         np.testing.assert_array_equal(life.gather_bits(), np.packbits(want, axis=1, bitorder="little"))
         assert life.gather_vtk() == gpu.vtk_bytes(want)
+
+
+@pytest.mark.parametrize("rccl", [None, "rank"], ids=["local", "rccl"])
+@pytest.mark.parametrize("kernel", ["bit", "byte"])
+@pytest.mark.parametrize("axes", [2, 3], ids=["x_only", "y_only"])
+@pytest.mark.parametrize("nx,ny,gens", [(512, 300, 70), (257, 131, 37), (4096, 400, 45)])
+def test_loopback_one_axis(gpu, oracle, nx, ny, gens, kernel, rccl, axes):
+    """LIFE_OPT_LOOPBACK 2 / 3: only x (as N = 2's {2, 1} blocks) or only y
+    goes through the transport, the other axis wraps in the stencil (or its
+    own apron copy for a width that is not a whole number of lane columns)."""
+    g0 = oracle.fill_random(nx, ny, seed=23, density=0.45)
+    want = oracle.life_run(g0, gens)
+    with _make(gpu, nx, ny, kernel, rccl) as life:
+        life.upload(g0)
+        life.configure(gpu.OPT_LOOPBACK, axes)
+        split = gens // 3
+        life.step(split)
+        life.step(gens - split)
+        np.testing.assert_array_equal(life.gather(), want)
