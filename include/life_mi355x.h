@@ -315,18 +315,6 @@ int life_dev_set_timing(life_dev *d, int on);
  * first pass that needs them.  Every life_dev_configure call waits for the
  * device (life_dev_sync). */
 #define LIFE_OPT_DEEP_HALO 9
-/* LIFE_OPT_INTERIOR_GRID (partitioned bit shards, the overlapped exchange
- * pass): how the interior tiles -- beside which the ring's halo (pack,
- * ncclSend / ncclRecv, unpack) runs -- are launched.  -r (default -8, or
- * -LIFE_PERSIST_RESERVE from the environment): a persistent launch of the
- * resident tile slots minus r workgroups that pull the tiles from per-XCD
- * queues, leaving r slots to the halo's kernels (one workgroup per tile fills
- * every slot a tile frees until its last tile is dispatched, and the RCCL
- * kernel then waits: 14 us alone, ~300 us beside a 65536^2 interior,
- * DESIGN.md §6); n > 0: a persistent launch of n workgroups (tests); 0: one
- * workgroup per tile.  A launch with no more tiles than that runs one
- * workgroup per tile either way.  Multiples of 8 (the XCDs).  Same results. */
-#define LIFE_OPT_INTERIOR_GRID 11
 /* Option 10 (LIFE_OPT_SKEW, time-skewed ghost-free tiles) was retired in
  * round 5: 8 % slower per launch on MI355X; it now fails
  * with LIFE_EINVAL like any unknown option. */

@@ -103,8 +103,6 @@ struct Shard {
     bool flow_used = false;  // a dataflow launch since the last sync checked its error word
     std::vector<life_halo_op> plan;
     bool corners = false;  // the plan exchanges the four corner blocks itself (fused, one phase)
-    unsigned int *qhead = nullptr;  // persistent interior tiles: 8 per-XCD counters (life::PersistTiles)
-    uint32_t qbase[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     std::vector<TimedLaunch> timers;
     size_t timers_used = 0;
     std::vector<PhaseEvents> phases;
@@ -184,17 +182,6 @@ static bool stream_priorities() {
     }();
     return v;
 }
-// LIFE_PERSIST_RESERVE (default 8; 0: the ordinary one-workgroup-per-tile
-// launch) sets LIFE_OPT_INTERIOR_GRID's default to -reserve at load time:
-// the exchange block's interior tiles as a persistent launch that leaves
-// that many resident slots free, so the halo's kernels, queued behind the
-// ring, find a slot at once instead of after the interior's last tile
-// (life_kernels.hip, tstep_bit_persist_kernel).
-static const int kEnvPersistReserve = [] {
-    const char *e = getenv("LIFE_PERSIST_RESERVE");
-    const int r = e ? atoi(e) : 8;
-    return r >= 0 && r <= 256 ? r : 8;
-}();
 static const int kEnvTimingMode = [] {
     const char *e = getenv("LIFE_TIMING_MODE");
     const int v = e ? atoi(e) : 0;
@@ -223,7 +210,6 @@ struct life_dev {
     int flow = kEnvFlow;  // LIFE_OPT_FLOW: single-shard bit tiles as one persistent dataflow launch per
                           // step call (1: write-through hand-off, 2: plain stores + release; 0 off)
     int64_t flow_chunk = 0;  // LIFE_OPT_FLOW_CHUNK: passes per dataflow launch at most (0: automatic)
-    int interior_grid = -kEnvPersistReserve;  // LIFE_OPT_INTERIOR_GRID (life::PersistTiles::grid)
     TimedLaunch *call_timer = nullptr;  // kTimeCall: the pair bracketing the current step call
     std::vector<Shard> shards;
     double acc_ms = 0.0;
@@ -293,8 +279,6 @@ int shard_alloc(life_dev *d, Shard &s) {
     HIPCHK(hipMalloc(&s.col_recv, col_bytes));
     HIPCHK(hipMalloc(&s.d_count, 2 * sizeof(unsigned long long)));
     HIPCHK(hipMalloc(&s.sink, 1024));
-    HIPCHK(hipMalloc(&s.qhead, 8 * sizeof(unsigned int)));
-    HIPCHK(hipMemsetAsync(s.qhead, 0, 8 * sizeof(unsigned int), s.stream));
     HIPCHK(hipMemsetAsync(s.col_send, fill, col_bytes, s.stream));
     HIPCHK(hipMemsetAsync(s.col_recv, fill, col_bytes, s.stream));
     HIPCHK(hipMemsetAsync(s.d_count, 0, 2 * sizeof(unsigned long long), s.stream));
@@ -324,7 +308,6 @@ void shard_free(Shard &s) {
             if (e) (void)hipEventDestroy(e);
     for (uint8_t *p : {s.buf[0], s.buf[1], s.col_send, s.col_recv, s.sink, s.stage})
         if (p) (void)hipFree(p);
-    if (s.qhead) (void)hipFree(s.qhead);
     if (s.flow) (void)hipFree(s.flow);
     if (s.d_count) (void)hipFree(s.d_count);
     if (s.h_count) (void)hipHostFree(s.h_count);
@@ -624,13 +607,10 @@ int harvest_phases(life_dev *d) {
 
 bool temporal(const life_dev *d) { return d->shards[0].lay.generations_per_exchange > 1; }
 
-
 // Launches up to 4 tile regions of the temporal stencil as ONE kernel on
-// `st` (m generations, cur -> nxt), optionally timed; `persist`: the
-// persistent form (launch_tstep's PersistTiles) when the launch has more
-// items than it leaves slots.
+// `st` (m generations, cur -> nxt), optionally timed.
 int launch_tiles(life_dev *d, Shard &s, const life::TileRegion *r, int nreg, int m, bool timed, hipStream_t st,
-                 life::Extend ext_ = life::Extend{}, bool persist = false) {
+                 life::Extend ext_ = life::Extend{}) {
     const uint8_t *in = s.buf[s.cur];
     uint8_t *out = s.buf[s.cur ^ 1];
     TimedLaunch *t = nullptr;
@@ -643,12 +623,8 @@ int launch_tiles(life_dev *d, Shard &s, const life::TileRegion *r, int nreg, int
     const life::Extend xt = ext_;
     const bool ext = ev && (kEnvTimingMode == kTimeExt || kEnvTimingMode == kTimeCall);
     if (ev && !ext) HIPCHK(hipEventRecord(t->a, st));
-    life::PersistTiles pt;
-    pt.qhead = s.qhead;
-    pt.qbase = s.qbase;
-    pt.grid = d->interior_grid;
     HIPCHK(life::launch_tstep(s.lay, in, out, r, nreg, m, wrap_of(d), st, &valu, ext ? t->a : nullptr,
-                              ext ? t->b : nullptr, xt, persist ? &pt : nullptr));
+                              ext ? t->b : nullptr, xt));
     if (ev && !ext) HIPCHK(hipEventRecord(t->b, st));
     if (d->timing && timed && t) {  // (no timer counts it -- span-only timing, LIFE_TIMING_MODE=3: no booking)
         const life::TileGeom g = life::tile_geom(life::extended_layout(s.lay, xt), m);
@@ -856,7 +832,7 @@ int generation_block(life_dev *d, int m, bool last) {
         for (int k = 0; k < n; k++) items += life::region_items(g, ring[k]);
         halo_side[si] = carry_on_halo_side(items, life::tile_slots(s.lay)) ? 1 : 0;
         if (pe[si]) HIPCHK(hipEventRecord(pe[si]->int0, s.stream2));
-        if (rb > ra && cb > ca) CHK(launch_tiles(d, s, &inner, 1, m, true, s.stream2, life::Extend{}, true));
+        if (rb > ra && cb > ca) CHK(launch(&inner, 1, true, s.stream2));
         if (pe[si]) HIPCHK(hipEventRecord(pe[si]->int1, s.stream2));
     }
     if (!(rx || ry)) {
@@ -1797,10 +1773,6 @@ int life_dev_configure(life_dev *d, int option, int value) {
         // (ADVICE r5): the call is collective there and checks agreement.
         if (d->rank_mode && d->world > 1) CHK(agree_all_ranks(d, value, "LIFE_OPT_DEEP_HALO"));
         d->deep = value != 0;
-        return LIFE_OK;
-    case LIFE_OPT_INTERIOR_GRID:
-        if (value < -256 || value > 1 << 20) return LIFE_EINVAL;
-        d->interior_grid = value;
         return LIFE_OK;
     case LIFE_OPT_FLOW_CHUNK:
         if (value < 0) return LIFE_EINVAL;

@@ -113,21 +113,10 @@ struct Extend {
 // Up to 4 disjoint tile regions in one launch; *valu_lane_ops (optional):
 // the modelled VALU lane-ops of the launch as tiled (tstep_valu_per_tile_lane).
 // Regions are in tile coordinates of tile_geom(extended_layout(L, ext), m).
-// Persistent form of a bit tile launch (tstep_bit_persist_kernel): `grid`
-// resident workgroups (< 0: the resident slots minus -grid, the slots left to
-// kernels queued beside it; > 0: that many; rounded down to a multiple of 8,
-// used only when the launch has more items) pull the launch's items from 8
-// per-XCD counters (qhead, device, 8 words zeroed once); qbase (host, 8
-// entries) is the counters' value before the launch and is advanced past it.
-struct PersistTiles {
-    unsigned int *qhead = nullptr;
-    uint32_t *qbase = nullptr;
-    int grid = -8;
-};
 hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, const TileRegion *r, int nreg,
                         int m, Wrap wrap, hipStream_t s,
                         double *valu_lane_ops = nullptr, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr,
-                        Extend ext = Extend{}, PersistTiles *pt = nullptr);
+                        Extend ext = Extend{});
 // The layout a deep-halo pass tiles: h + 2 ext.y rows starting ext.y rows
 // into the top apron.
 life_layout extended_layout(const life_layout &L, const Extend &ext);

@@ -310,11 +310,6 @@ struct TArgs {
     // deep-halo pass (Extend::x, bit): the lanes holding the apron pairs -1
     // and W store them too
     int32_t xext;
-    // persistent form (tstep_bit_persist_kernel): `items` workgroup items
-    // pulled from 8 per-XCD counters at qhead, each offset by qbase
-    int64_t items;
-    unsigned int *qhead;
-    uint32_t qbase[8];
 };
 
 template <int NW>
@@ -432,7 +427,7 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             uint64_t q;
-            if (FLOW == 1 || FLOW == 2)
+            if (FLOW)
                 q = __hip_atomic_load(reinterpret_cast<uint64_t *>(const_cast<uint8_t *>(p) + voff),
                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             else
@@ -487,7 +482,7 @@ __device__ __forceinline__ void tile_body_bit(const TArgs &a, const uint8_t *in,
             ve[0] = BitEnc::rule1(ae0, ae1, pe0, pe1, ce0, ce1, ve[0]);
             vo[0] = BitEnc::rule1(ao0, ao1, po0, po1, co0, co1, vo[0]);
         }
-        constexpr int BAH = FLOW ? LIFE_FLOW_BP_AHEAD : 0;  // permutes ahead (dataflow / persistent tiles)
+        constexpr int BAH = FLOW ? LIFE_FLOW_BP_AHEAD : 0;  // permutes ahead (dataflow tiles only)
         uint32_t bl[BAH > 0 ? BAH : 1], br[BAH > 0 ? BAH : 1];
 #pragma unroll
         for (int k = 0; k < BAH; ++k)
@@ -741,38 +736,6 @@ __device__ __forceinline__ void tile_body_byte(const TArgs &a, const uint8_t *in
 // (R = 16) or 1 at 128.
 constexpr int bit_wpe(int NW, int R) { return NW == 16 ? (R <= 16 ? 8 : 4) : (R <= 24 ? 6 : 4); }
 
-// Workgroup item wg of a tile launch: a half-height tail tile, a tile of one
-// of the regions, or a banded item of the last tile column.
-// F: tile_body_bit's FLOW argument -- 0 for the one-shot launch, 3 for the
-// persistent one (plain loads and stores, permutes issued ahead as in the
-// dataflow tiles: inside an item loop the compiler again put every permute
-// right before its wait, mean distance 1.8 instructions).
-template <int R, bool WRAPX, bool WRAPY, int NW, int F = 0>
-__device__ __forceinline__ void tstep_item(const TArgs &a, int64_t wg, XchB<NW> &xch) {
-    if (a.half_first > 0 && wg >= a.half_first) {
-        const int64_t i = wg - a.half_first;
-        tile_body_bit<R / 2, WRAPX, WRAPY, F, NW>(a, a.in, a.out, i % a.half_ntx, i / a.half_ntx, xch, 6, 1,
-                                                  a.half_y, a.half_yend);
-        return;
-    }
-    const int64_t nwg = a.first[a.nreg];
-    if (wg >= nwg) return;  // whole workgroup
-    int k = 0;
-    while (k + 1 < a.nreg && wg >= a.first[k + 1]) ++k;
-    const int64_t wr = wg - a.first[k];
-    const bool bands = a.gsh < 6 && a.tx1[k] == a.bcol + 1;
-    const int64_t ntx = a.tx1[k] - a.tx0[k] - (bands ? 1 : 0);
-    const int64_t nfull = ntx * (a.ty1[k] - a.ty0[k]);
-    if (wr < nfull) {
-        const int64_t tx = a.tx0[k] + wr % ntx, ty = a.ty0[k] + wr / ntx;
-        tile_body_bit<R, WRAPX, WRAPY, F, NW>(a, a.in, a.out, tx, ty, xch);
-    } else {
-        const int64_t B = 64 >> a.gsh, ty = a.ty0[k] + (wr - nfull) * B;
-        const int nb = (int)(a.ty1[k] - ty < B ? a.ty1[k] - ty : B);
-        tile_body_bit<R, WRAPX, WRAPY, F, NW, true>(a, a.in, a.out, a.bcol, ty, xch, a.gsh, nb);
-    }
-}
-
 // One workgroup per tile (or banded item / half-height tail tile).
 template <int R, bool WRAPX, bool WRAPY, int NW>
 __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tstep_bit_kernel(TArgs a) {
@@ -787,49 +750,30 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tstep_bit_kernel(TArg
         const int64_t n = a.xcd_n, x = wg & 7, k = wg >> 3, per = n >> 3, rem = n & 7;
         wg = (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + k;
     }
-    tstep_item<R, WRAPX, WRAPY, NW>(a, wg, xch);
-    wg_trace(1);
-}
-
-// The same items from fewer resident workgroups than the chip holds
-// (launch_tstep, PersistTiles): workgroup b pulls from counter b % 8 -- its
-// XCD's -- the XCD-contiguous run of items tstep_bit_kernel gives that XCD,
-// then every 8th item past them (half-height tail tiles).  The slots it
-// leaves free let kernels queued beside it (the exchange block's pack / RCCL
-// / unpack behind the ring) start at once: a full chip of tiles leaves no
-// slot an RCCL workgroup fits into until its last tiles are dispatched
-// (profiles/r05/w, xb: the RCCL kernel ended within 5 us of the interior,
-// 14 us when alone).
-template <int R, bool WRAPX, bool WRAPY, int NW>
-__global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tstep_bit_persist_kernel(TArgs a0) {
-    __shared__ XchB<NW> xch;
-    __shared__ uint32_t pull_sh;
-    for (;;) {
-        // the kernel arguments re-read per item: hoisted out of the item loop,
-        // the regions, buffers and queue ranges stayed live in SGPRs across
-        // the generation loop (104-106 SGPRs, VGPR spills, scratch, a late
-        // dispatch and a 15 % slower interior: profiles/r05/xc)
-        // Round 6: read through the kernarg segment pointer (constant address
-        // space: scalar loads), made opaque per item so the loads cannot be
-        // hoisted.  Taking the address of the by-value parameter instead
-        // copied the 300-byte TArgs to scratch (private segment 384-400 B,
-        // 13-17 VGPR spills: the round-5 attempt's 13-15 % loss).
-        typedef __attribute__((address_space(4))) const TArgs KArgs;
-        KArgs *kp = (KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
-        asm volatile("" : "+s"(kp));
-        const TArgs &a = *(const TArgs *)kp;
-        (void)a0;
-        const int64_t q = blockIdx.x & 7;
-        if (threadIdx.x == 0) pull_sh = atomicAdd(a.qhead + q, 1u) - a.qbase[q];
-        __syncthreads();
-        const int64_t nf = a.xcd_n, per = nf >> 3, rem = nf & 7;
-        const int64_t nfq = per + (q < rem ? 1 : 0), nh = a.items - nf, nhq = nh > q ? (nh - q + 7) / 8 : 0;
-        const int64_t i = (int64_t)__builtin_amdgcn_readfirstlane(pull_sh);
-        if (i >= nfq + nhq) return;  // the whole workgroup leaves
-        const int64_t lo = q < rem ? q * (per + 1) : rem * (per + 1) + (q - rem) * per;
-        tstep_item<R, WRAPX, WRAPY, NW, 3>(a, i < nfq ? lo + i : nf + q + 8 * (i - nfq), xch);
-        __syncthreads();  // the exchange slots and pull_sh are reused by the next item
+    if (a.half_first > 0 && wg >= a.half_first) {
+        const int64_t i = wg - a.half_first;
+        tile_body_bit<R / 2, WRAPX, WRAPY, 0, NW>(a, a.in, a.out, i % a.half_ntx, i / a.half_ntx, xch, 6, 1,
+                                                  a.half_y, a.half_yend);
+        wg_trace(1);
+        return;
     }
+    const int64_t nwg = a.first[a.nreg];
+    if (wg >= nwg) return;  // whole workgroup
+    int k = 0;
+    while (k + 1 < a.nreg && wg >= a.first[k + 1]) ++k;
+    const int64_t wr = wg - a.first[k];
+    const bool bands = a.gsh < 6 && a.tx1[k] == a.bcol + 1;
+    const int64_t ntx = a.tx1[k] - a.tx0[k] - (bands ? 1 : 0);
+    const int64_t nfull = ntx * (a.ty1[k] - a.ty0[k]);
+    if (wr < nfull) {
+        const int64_t tx = a.tx0[k] + wr % ntx, ty = a.ty0[k] + wr / ntx;
+        tile_body_bit<R, WRAPX, WRAPY, 0, NW>(a, a.in, a.out, tx, ty, xch);
+    } else {
+        const int64_t B = 64 >> a.gsh, ty = a.ty0[k] + (wr - nfull) * B;
+        const int nb = (int)(a.ty1[k] - ty < B ? a.ty1[k] - ty : B);
+        tile_body_bit<R, WRAPX, WRAPY, 0, NW, true>(a, a.in, a.out, a.bcol, ty, xch, a.gsh, nb);
+    }
+    wg_trace(1);
 }
 
 template <int R, int GK, bool WRAPX, bool WRAPY, int NW>
@@ -1854,22 +1798,6 @@ const void *bit_k(Wrap wrap) {
     return nullptr;
 }
 const void *tstep_bit_fn() { return bit_k(Wrap{true, true}); }
-// the persistent tiles: partitioned shards only (an axis with an apron)
-template <int R, int NW>
-const void *bit_persist_fn(Wrap wrap) {
-    if (wrap.x && wrap.y) return nullptr;
-    if (wrap.x) return (const void *)tstep_bit_persist_kernel<R, true, false, NW>;
-    if (wrap.y) return (const void *)tstep_bit_persist_kernel<R, false, true, NW>;
-    return (const void *)tstep_bit_persist_kernel<R, false, false, NW>;
-}
-const void *bit_persist_k(Wrap wrap) {
-    const int R = temporal_rows(true), NW = tile_waves(true);
-#define LIFE_BIT_CASE(r, nw) \
-    if (R == r && NW == nw) return bit_persist_fn<r, nw>(wrap);
-    LIFE_BIT_SHAPES(LIFE_BIT_CASE)
-#undef LIFE_BIT_CASE
-    return nullptr;
-}
 }  // namespace
 
 // Byte tiles are compiled for a fixed ghost depth (a runtime depth measured
@@ -2016,7 +1944,7 @@ life_layout extended_layout(const life_layout &L, const Extend &ext) {
 
 hipError_t launch_tstep(const life_layout &Lin, const uint8_t *in, uint8_t *out, const TileRegion *r, int nreg,
                         int m, Wrap wrap, hipStream_t s, double *valu_lane_ops, hipEvent_t ev0, hipEvent_t ev1,
-                        Extend ext, PersistTiles *pt) {
+                        Extend ext) {
     const int K = Lin.generations_per_exchange;
     const bool bit = is_bit(Lin);
     // m <= 32: the tile's edge lanes absorb at most 32 wrong cells; m <= the
@@ -2117,28 +2045,6 @@ hipError_t launch_tstep(const life_layout &Lin, const uint8_t *in, uint8_t *out,
         *valu_lane_ops = (double)(a.half_first > 0 ? a.half_first : items) * 64.0 * tstep_valu_per_tile_lane(m, !bit);
         if (a.half_first > 0)  // half tiles: R / 2 register rows per wave
             *valu_lane_ops += (double)(items - a.half_first) * 64.0 * 0.5 * tstep_valu_per_tile_lane(m, !bit);
-    }
-    if (pt && bit && pt->qhead && pt->qbase && pt->grid != 0) {
-        // persistent: leave -grid slots to the kernels queued beside it (or
-        // run on `grid` workgroups)
-        const int64_t slots = tstep_bit_slots();
-        const int64_t want = pt->grid < 0 ? slots + pt->grid : std::min<int64_t>(pt->grid, slots);
-        const int64_t grid = (std::min<int64_t>(items, want) / 8) * 8;
-        const void *pfn = bit_persist_k(wrap);
-        if (pfn && grid >= 8 && grid < items) {
-            a.items = items;
-            a.qhead = pt->qhead;
-            for (int q = 0; q < 8; q++) a.qbase[q] = pt->qbase[q];
-            const hipError_t e = launch_fn(pfn, (unsigned)grid, 64u * (unsigned)tile_waves(true), &a, s, ev0, ev1);
-            if (e != hipSuccess) return e;
-            // every workgroup of queue q pulls once past its items
-            const int64_t nf = a.xcd_n, per = nf >> 3, rem = nf & 7, nh = items - nf;
-            for (int q = 0; q < 8; q++) {
-                const int64_t nfq = per + (q < rem ? 1 : 0), nhq = nh > q ? (nh - q + 7) / 8 : 0;
-                pt->qbase[q] += (uint32_t)(nfq + nhq + grid / 8);
-            }
-            return hipSuccess;
-        }
     }
     const void *fn = bit                      ? bit_k(wrap)
                      : byte_one_ghost(L, m) ? byte_fn<48, 1>(wrap)

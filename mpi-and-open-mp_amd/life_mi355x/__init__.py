@@ -44,7 +44,6 @@ HALO_COLUMN, HALO_ROW, HALO_CORNER = 0, 1, 2
 OPT_SMALL_GRID, OPT_OVERLAP, OPT_SMALL_WINDOW, OPT_BLOCK_GENS, OPT_LOOPBACK, OPT_FLOW = 1, 2, 4, 5, 6, 7
 OPT_FLOW_CHUNK = 8
 OPT_DEEP_HALO = 9
-OPT_INTERIOR_GRID = 11
 # LIFE_TEMPORAL_DEPTH(_BYTE): generations per halo exchange of the temporal layouts
 TEMPORAL_DEPTH = {"bit": 32, "byte": 32}
 BLOCK_GENS = {"bit": 12, "byte": 32}  # tiles: default generations per launch at most (LIFE_OPT_BLOCK_GENS)

@@ -17,7 +17,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def run_bench(*args):
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", *args],
+    # more shards than this box has GPUs: an explicit rehearsal
+    extra = ["--rehearse-shards"] if "--gpus" in args else []
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", *extra, *args],
                        capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -29,7 +31,11 @@ def run_bench(*args):
 def test_strong_scaling_4_shards_full_size(kernel):
     """configs[3] at N = 4: 65536^2 split 2x2 (MPI_Dims_create), LOCAL shards."""
     out = run_bench("--gpus", "4", "--scaling", "strong", "--kernel", kernel, "--steps", "40", "--warmup", "8")
-    assert out["scaling"] == "strong" and out["n_gpus"] == 4
+    assert out["scaling"] == "strong"
+    # a rehearsal says what it ran on: one GPU, four shards, no RCCL communicator (LOCAL copies)
+    c = out["config"]
+    assert out["n_gpus"] == 1 and c["shards"] == 4 and c["devices"] == 1 and c["rehearsal"] is True, c
+    assert c["rccl_nranks"] == 0 and len(c["pci_bus_ids"]) == 1, c
     assert out["config"]["dims"] == [2, 2] and out["config"]["nx"] == out["config"]["ny"] == 65536
     p = out["parity_vs_1gpu"]
     assert p["ok"] is True and p["live"] > 0, p
@@ -85,5 +91,6 @@ def test_single_gpu_line_is_valu_roofline():
     assert r["issued"]["ops_per_launch"] > r["algorithmic_ops_per_launch"] and r["issued"]["frac"] > r["frac"]
     assert r["hbm"]["achieved"] > 0 and r["hbm"]["peak"] == 8000.0
     assert "parity_vs_1gpu" not in out and out["scaling"] == "weak"
+    assert out["n_gpus"] == 1 and out["config"]["shards"] == 1 and out["config"]["rehearsal"] is False
     c = out["call"]  # one event pair around the call's launches: span <= the bench clock
     assert c["passes"] == 3 and 0 < c["device_span_ms"] <= c["elapsed_ms"] and c["host_enqueue_ms"] > 0, c

@@ -169,37 +169,3 @@ def test_loopback_one_axis(gpu, oracle, nx, ny, gens, kernel, rccl, axes):
         life.step(split)
         life.step(gens - split)
         np.testing.assert_array_equal(life.gather(), want)
-
-
-@pytest.mark.parametrize("grid", [8, 16, -8, 0], ids=["persist8", "persist16", "reserve8", "one_shot"])
-@pytest.mark.parametrize("rccl", [None, "rank"], ids=["local", "rccl"])
-def test_persistent_interior(gpu, oracle, rccl, grid):
-    """LIFE_OPT_INTERIOR_GRID (round 6): the exchange
-    pass's interior tiles as a persistent launch whose workgroups pull the
-    tiles from per-XCD queues -- 8 / 16 workgroups for 66 interior items
-    (banded last tile column included), the default (slots - 8: one-shot
-    here, too few items), and the one-workgroup-per-tile launch.  Several
-    exchange blocks per call, the queues' epoch counters carried across
-    launches and calls."""
-    nx, ny, gens = 16384, 4096, 100
-    g0 = oracle.fill_random(nx, ny, seed=31, density=0.5)
-    want = oracle.life_run(g0, gens, threads=8)
-    with _make(gpu, nx, ny, "bit", rccl) as life:
-        life.upload(g0)
-        life.configure(gpu.OPT_LOOPBACK, 1)
-        life.configure(gpu.OPT_INTERIOR_GRID, grid)
-        life.step(37)
-        life.step(gens - 37)
-        np.testing.assert_array_equal(life.gather(), want)
-
-
-def test_persistent_interior_local_shards(gpu, oracle):
-    """Two LOCAL shards ({2, 1}: x partitioned, y wrapped in the stencil),
-    each shard's interior on 8 persistent workgroups, deep halo on."""
-    nx, ny, gens = 32768, 2048, 70
-    g0 = oracle.fill_random(nx, ny, seed=41, density=0.5)
-    with gpu.Life(nx, ny, shards=2, kernel="bit", dims=(2, 1), transport=gpu.XPORT_LOCAL) as life:
-        life.configure(gpu.OPT_INTERIOR_GRID, 8)
-        life.upload(g0)
-        life.step(gens)
-        np.testing.assert_array_equal(life.gather(), oracle.life_run(g0, gens, threads=8))

@@ -48,6 +48,8 @@ def test_bench_rank_mode_torchrun():
     assert len(lines) == 1, p.stdout
     out = json.loads(lines[0])
     assert out["n_gpus"] == 1 and out["value"] > 0
+    # the line names its RCCL communicator: one rank (world 1, an id was broadcast), one device
+    assert out["config"]["rccl_nranks"] == 1 and out["config"]["devices"] == 1, out["config"]
     # same grid, same generations as the single-process form
     import oracle as O
 

@@ -129,18 +129,13 @@ def test_byte_permutes_issued_ahead(isa):
 FLOW_KERNEL = "tflow_kernel<24, true, true, 1, 8, false>"  # the dataflow form (write-through hand-off)
 
 
-PERSIST_KERNEL = "tstep_bit_persist_kernel<24, false, false, 8>"  # the partitioned interior's instance
-
-
-@pytest.mark.parametrize("kernel", [FLOW_KERNEL, PERSIST_KERNEL], ids=["dataflow", "persistent"])
-def test_flow_permutes_issued_ahead(isa, kernel):
-    """The dataflow tiles' and the persistent tiles' generation loops issue
-    each row's two permutes one row ahead (LIFE_FLOW_BP_AHEAD = 1): their
-    waits leave the next row's two (and the current row's second) in flight
-    -- lgkmcnt(2) / (3).  Left to the compiler, every permute sat right before
-    its wait inside an item loop (mean distance 1.8 instructions against
-    7.6-9.8 in the one-shot tiles)."""
-    lines = kernel_lines(isa[0], kernel)
+def test_flow_permutes_issued_ahead(isa):
+    """The dataflow tiles' generation loop issues each row's two permutes one
+    row ahead (LIFE_FLOW_BP_AHEAD = 1): its waits leave the next row's two
+    (and the current row's second) in flight -- lgkmcnt(2) / (3).  Left to
+    the compiler, every permute sat right before its wait there (mean
+    distance 1.8 instructions against 7.6-9.8 in the per-launch tiles)."""
+    lines = kernel_lines(isa[0], FLOW_KERNEL)
     loops = []
     for addr, op, text in lines:
         m = re.match(r"s_cbranch_\w+ (\d+)$", text)
@@ -151,7 +146,7 @@ def test_flow_permutes_issued_ahead(isa, kernel):
         ops = [t.split()[0] for t in body]
         if "s_barrier" in ops and ops.count("v_bitop3_b32") == 480:
             loops.append(body)
-    assert loops, f"no generation loop found in {kernel}"
+    assert loops, "no dataflow generation loop found"
     for body in loops:
         ahead = sum(1 for t in body if t in ("s_waitcnt lgkmcnt(2)", "s_waitcnt lgkmcnt(3)"))
         assert ahead >= 40, f"{ahead} waits with permutes of the next row in flight"
