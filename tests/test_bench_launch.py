@@ -8,6 +8,8 @@ import os
 import subprocess
 import sys
 
+import torch  # noqa: F401  (before any test loads liblife_mi355x: the gloo test spawns through torch)
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 PARENT = """
