@@ -983,6 +983,20 @@ int create_common(life_dev *d, const std::vector<int> &ranks, const std::vector<
 
 static int flow_prewarm(life_dev *d);
 
+// The launch-tail plans (life::tail_plan) of the passes this device's step
+// calls will launch, computed up front: a plan's first search costs ~50 us of
+// host time, which a timed call's first launch would otherwise wait for
+// (deep-halo passes: every extension 0 .. K - m).
+static void tail_prewarm(const life_dev *d) {
+    const int mmax = d->block_gens > 0 ? d->block_gens : 12;
+    for (size_t i = 0; i < d->shards.size(); ++i) {
+        bool seen = false;  // identical blocks share their plans (cached by shape)
+        for (size_t j = 0; j < i; ++j)
+            seen |= d->shards[j].lay.w == d->shards[i].lay.w && d->shards[j].lay.h == d->shards[i].lay.h;
+        if (!seen) life::prewarm_tail_plans(d->shards[i].lay, mmax, part(d, 1));
+    }
+}
+
 extern "C" {
 
 const char *life_last_error(void) { return g_err.c_str(); }
@@ -1056,6 +1070,7 @@ int life_dev_create_ex(int64_t nx, int64_t ny, int nshards, int dims0, int dims1
     }
     // not fatal: the first dataflow call allocates and launches as it would
     if (flow_prewarm(d) != LIFE_OK) (void)hipGetLastError();
+    tail_prewarm(d);
     *out = d;
     return LIFE_OK;
 }
@@ -1113,6 +1128,7 @@ int life_dev_create_rank(int64_t nx, int64_t ny, int kernel, int rank, int world
     }
     // not fatal: the first dataflow call allocates and launches as it would
     if (flow_prewarm(d) != LIFE_OK) (void)hipGetLastError();
+    tail_prewarm(d);
     *out = d;
     return LIFE_OK;
 }
@@ -1759,6 +1775,7 @@ int life_dev_configure(life_dev *d, int option, int value) {
     case LIFE_OPT_BLOCK_GENS:
         if (value < 0 || value > 32) return LIFE_EINVAL;
         d->block_gens = value > 0 ? value : default_block_gens(d->kernel);
+        tail_prewarm(d);
         return LIFE_OK;
     case LIFE_OPT_FLOW:
         if (value < 0 || value > 3) return LIFE_EINVAL;
@@ -1809,6 +1826,7 @@ int life_dev_configure(life_dev *d, int option, int value) {
         s.corners =
             std::any_of(s.plan.begin(), s.plan.end(), [](const life_halo_op &o) { return o.what == LIFE_HALO_CORNER; });
         CHK(exchange(d, 0, false));
+        tail_prewarm(d);
         return life_dev_sync(d);
     }
     default: return LIFE_EINVAL;

@@ -117,6 +117,12 @@ hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, c
                         int m, Wrap wrap, hipStream_t s,
                         double *valu_lane_ops = nullptr, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr,
                         Extend ext = Extend{});
+// Computes (and caches) the launch-tail plans launch_tstep will use for the
+// whole-shard launches of layout L at m = 1 .. mmax generations (with
+// ext_y: also every deep-halo extension 0 .. K - m), so that a step call
+// does not pay the planner's search (~50 us per new shape) before its first
+// launch.
+void prewarm_tail_plans(const life_layout &L, int mmax, bool ext_y);
 // The layout a deep-halo pass tiles: h + 2 ext.y rows starting ext.y rows
 // into the top apron.
 life_layout extended_layout(const life_layout &L, const Extend &ext);

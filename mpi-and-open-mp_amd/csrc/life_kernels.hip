@@ -298,11 +298,15 @@ struct TArgs {
     // ceil((ty1 - ty0) / (64 / G)) banded items
     int32_t gsh;
     int64_t bcol;
-    // tail split (bit, one launch of one full-width region): workgroups >=
-    // half_first run half-height tiles (R / 2 rows per wave) over rows
-    // [half_y, half_yend), half_ntx per tile row, so the last round of a
-    // launch is made of half-length items (launch_tstep)
-    int64_t half_first, half_y, half_ntx, half_yend;
+    // tail split (bit, one launch of one full-width region; launch_tstep):
+    // workgroups [sec_first[0], sec_first[1]) run 3/4-height tiles (3R / 4
+    // rows per wave) over owned rows [sec_y[0], sec_y[1]), workgroups
+    // [sec_first[1], sec_first[2]) half-height tiles (R / 2 rows per wave)
+    // over rows [sec_y[1], sec_y[2]); each section's tile rows span all ntx
+    // tile columns, the last one banded like the full tiles (gsh < 6).  The
+    // last rounds of a launch are then shorter items that fill the slots the
+    // full tiles leave.  sec_first[2] == 0: no split.
+    int64_t sec_first[3], sec_y[3], sec_ntx;
     // XCD-aware order (bit, LIFE_XCD_ORDER): workgroups [0, xcd_n) are
     // renumbered so that each XCD (blocks b, b + 8, ... share one) walks a
     // contiguous row-major run of items; 0: dispatch order
@@ -736,7 +740,26 @@ __device__ __forceinline__ void tile_body_byte(const TArgs &a, const uint8_t *in
 // (R = 16) or 1 at 128.
 constexpr int bit_wpe(int NW, int R) { return NW == 16 ? (R <= 16 ? 8 : 4) : (R <= 24 ? 6 : 4); }
 
-// One workgroup per tile (or banded item / half-height tail tile).
+// Item i of a tail section (TArgs::sec_*): RS rows per wave, tile rows of
+// TS = NW RS - 2m owned rows from owned row y0, the last one stopping at
+// yend; ntx - 1 ordinary tiles per tile row, then the banded items of the
+// last tile column (B = 64 >> gsh tile rows each), or ntx tiles per row.
+template <int RS, bool WRAPX, bool WRAPY, int NW>
+__device__ __forceinline__ void tail_item(const TArgs &a, int64_t i, int64_t y0, int64_t yend, XchB<NW> &xch) {
+    const int64_t TS = (int64_t)NW * RS - 2 * a.m;
+    const int64_t rows = (yend - y0 + TS - 1) / TS;
+    const bool band = a.gsh < 6;
+    const int64_t ntxs = a.sec_ntx - (band ? 1 : 0), nfull = ntxs * rows;
+    if (i < nfull) {
+        tile_body_bit<RS, WRAPX, WRAPY, 0, NW>(a, a.in, a.out, i % ntxs, i / ntxs, xch, 6, 1, y0, yend);
+    } else {
+        const int64_t B = 64 >> a.gsh, ty = (i - nfull) * B;
+        const int nb = (int)(rows - ty < B ? rows - ty : B);
+        tile_body_bit<RS, WRAPX, WRAPY, 0, NW, true>(a, a.in, a.out, a.bcol, ty, xch, a.gsh, nb, y0, yend);
+    }
+}
+
+// One workgroup per tile (or banded item / partial-height tail tile).
 template <int R, bool WRAPX, bool WRAPY, int NW>
 __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tstep_bit_kernel(TArgs a) {
     __shared__ XchB<NW> xch;
@@ -750,10 +773,11 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tstep_bit_kernel(TArg
         const int64_t n = a.xcd_n, x = wg & 7, k = wg >> 3, per = n >> 3, rem = n & 7;
         wg = (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + k;
     }
-    if (a.half_first > 0 && wg >= a.half_first) {
-        const int64_t i = wg - a.half_first;
-        tile_body_bit<R / 2, WRAPX, WRAPY, 0, NW>(a, a.in, a.out, i % a.half_ntx, i / a.half_ntx, xch, 6, 1,
-                                                  a.half_y, a.half_yend);
+    if (a.sec_first[2] > 0 && wg >= a.sec_first[0]) {
+        if (wg < a.sec_first[1])
+            tail_item<R * 3 / 4, WRAPX, WRAPY, NW>(a, wg - a.sec_first[0], a.sec_y[0], a.sec_y[1], xch);
+        else
+            tail_item<R / 2, WRAPX, WRAPY, NW>(a, wg - a.sec_first[1], a.sec_y[1], a.sec_y[2], xch);
         wg_trace(1);
         return;
     }
@@ -1870,32 +1894,31 @@ static bool xcd_order_byte_enabled() {
     return on;
 }
 
-// LIFE_TAIL_SPLIT: 0 no half-height tail tiles, 1 the round-4 rule (the
+// LIFE_TAIL_SPLIT: 0 no partial-height tail tiles, 1 the round-4 rule (the
 // fewest bottom tile rows whose half tiles fill one round, when the last
-// round is under half full), 2 (default, round 5) the split a
-// list-scheduling model of the launch says ends first (tail_makespan).
+// round is under half full), 2 (round 5) the split with half tiles a
+// list-scheduling model of the launch says ends first, 3 (default, round 6)
+// the same model choosing among full, 3/4- and half-height tiles
+// (life::tail_plan, life_plan.cpp; scripts/tail_model.py restates it).
 static int tail_split_mode() {
     static const int v = [] {
         const char *e = getenv("LIFE_TAIL_SPLIT");
-        const int m = e ? atoi(e) : 2;
-        return m >= 0 && m <= 2 ? m : 2;
+        const int m = e ? atoi(e) : 3;
+        return m >= 0 && m <= 3 ? m : 3;
     }();
     return v;
 }
-// Length in full-tile times of a launch of `full` tiles then `half` tiles of
-// half the duration dealt in order to `slots` resident workgroups, rounds
-// ending together (scripts/tail_model.py): after r = full / slots rounds the
-// rem = full % slots last full tiles hold their slots one more unit while the
-// others take half tiles, two per unit.
-static double tail_makespan(int64_t full, int64_t half, int64_t slots) {
-    const int64_t r = full / slots, rem = full % slots;
-    if (half == 0) return (double)(r + (rem ? 1 : 0));
-    if (rem == 0) return (double)r + 0.5 * (double)((half + slots - 1) / slots);
-    const int64_t gap = 2 * (slots - rem);  // half tiles done in the last full round's idle slots
-    if (half <= gap) return (double)(r + 1);
-    return (double)(r + 1) + 0.5 * (double)((half - gap + slots - 1) / slots);
+// LIFE_TAIL_C (measurement knob, default 0.06): the fixed share of a tile's
+// duration (window load, stores, workgroup turnover) in the tail model's
+// item durations (life::tail_plan).
+static double tail_c() {
+    static const double v = [] {
+        const char *e = getenv("LIFE_TAIL_C");
+        const double c = e ? atof(e) : 0.06;
+        return c >= 0.0 && c < 1.0 ? c : 0.06;
+    }();
+    return v;
 }
-
 // resident workgroups of a kernel on this device (occupancy)
 static int slots_of(const void *fn, int threads) {
     int dev = 0, cus = 0, per = 0;
@@ -1942,6 +1965,28 @@ life_layout extended_layout(const life_layout &L, const Extend &ext) {
     return V;
 }
 
+// The tail plan of a full-width bit launch over tile rows [ty0, ty1) of
+// tile_geom(L, m) (launch_tstep; cached by life::tail_plan).
+static TailPlan tail_plan_for(const life_layout &L, const TileGeom &g, int m, int64_t ty0, int64_t ty1) {
+    const int Rb = temporal_rows(true), NWb = tile_waves(true), gh = tile_ghost(L, m);
+    const int64_t T34 = (int64_t)NWb * (Rb * 3 / 4) - 2 * gh, T2 = (int64_t)NWb * (Rb / 2) - 2 * gh;
+    const int64_t yend = std::min(ty1 * g.rows, L.h), B = g.gsh < 6 ? 64 >> g.gsh : 1;
+    return tail_plan(g.ntx, B, ty0, ty1, yend, g.rows, T34, T2, tstep_bit_slots(), tail_split_mode(), tail_c());
+}
+
+void prewarm_tail_plans(const life_layout &L, int mmax, bool ext_y) {
+    if (!is_bit(L) || L.generations_per_exchange < 2 || tail_split_mode() == 0) return;
+    const int K = L.generations_per_exchange;
+    for (int m = 1; m <= std::min(mmax, K); ++m)
+        for (int e = 0; e <= (ext_y ? K - m : 0); ++e) {
+            Extend x;
+            x.y = e;
+            const life_layout V = extended_layout(L, x);
+            const TileGeom g = tile_geom(V, m);
+            if (g.rows >= 1) (void)tail_plan_for(V, g, m, 0, g.nty);
+        }
+}
+
 hipError_t launch_tstep(const life_layout &Lin, const uint8_t *in, uint8_t *out, const TileRegion *r, int nreg,
                         int m, Wrap wrap, hipStream_t s, double *valu_lane_ops, hipEvent_t ev0, hipEvent_t ev1,
                         Extend ext) {
@@ -1982,69 +2027,46 @@ hipError_t launch_tstep(const life_layout &Lin, const uint8_t *in, uint8_t *out,
     }
     if (a.nreg == 0 || m <= 0) return hipSuccess;
     int64_t items = a.first[a.nreg];  // one workgroup per tile (or banded item)
-    a.half_first = a.half_y = a.half_ntx = a.half_yend = 0;
-    const int64_t T2 = (int64_t)tile_waves(bit) * (temporal_rows(bit) / 2) - 2 * (int64_t)tile_ghost(L, m);
+    for (int k = 0; k < 3; k++) a.sec_first[k] = a.sec_y[k] = 0;
+    a.sec_ntx = g.ntx;
+    const int Rb = temporal_rows(bit), NWb = tile_waves(bit), gh = tile_ghost(L, m);
+    const int64_t T34 = (int64_t)NWb * (Rb * 3 / 4) - 2 * gh, T2 = (int64_t)NWb * (Rb / 2) - 2 * gh;
     if (bit && T2 >= 1 && a.nreg == 1 && a.tx0[0] == 0 && a.tx1[0] == g.ntx && tail_split_mode() > 0) {
-        // one full-width region: the whole shard, or the interior of a row
-        // strip (rows [ra, rb) of tiles; the ring runs concurrently)
-        // The launch runs items / slots rounds of equal tiles; a last round
-        // under half full leaves most CUs idle for a whole tile time.
-        // Measured (profiles/r02/r2z): bit 20-generation calls +1.5-2 %; the
-        // byte tiles (2 per CU, 32 ghost rows: a third of a half tile) lost
-        // 3-4 %, so they keep whole tiles.
-        // Re-tile the bottom q tile rows as half-height tiles (R / 2 rows per
-        // wave, one round's worth or more): they are dispatched last, so the
-        // final round is half-length items on every slot.
-        const int slots = tstep_bit_slots();
-        const int64_t rem = slots > 0 ? items % slots : 0;
+        // One full-width region: the whole shard, a deep-halo pass over the
+        // extended shard, or the interior of a row strip (the ring runs
+        // concurrently).  The launch runs items / slots rounds of equal
+        // tiles; a last round under full leaves CUs idle for up to a whole
+        // tile time.  The bottom tile rows are re-tiled as 3/4- and
+        // half-height tiles, banded in the last column like the full tiles,
+        // dispatched last, so the final rounds are short items filling the
+        // idle slots (life::tail_plan; LIFE_TAIL_SPLIT 3, round 6; 2: half
+        // tiles only, round 5; 1: round 4's rule; 0: off).  The byte tiles
+        // (2 per CU, 32 ghost rows: a third of a half tile) lost 3-4 % with
+        // half tiles (profiles/r02/r2z) and keep whole tiles.
         const int64_t ty0 = a.ty0[0], ty1 = a.ty1[0], yend = std::min(ty1 * g.rows, L.h);
-        // (Splitting whatever the last round's fill measured 1-3 % slower,
-        // profiles/r04/tail_u.)
-        const int mode = tail_split_mode();
-        if (mode == 2 && slots > 0 && items > slots && rem != 0) {
-            // the bottom q tile rows as half tiles, q chosen by the model
-            // (65536^2 at m = 10: 8.5 tile-times against 9.0 for the rule
-            // of mode 1; ties keep more full tiles); q = 0: no split
-            double best = tail_makespan(items, 0, slots);
-            int64_t bq = 0;
-            for (int64_t q = 1; q < ty1 - ty0; ++q) {
-                const int64_t F = ty1 - q;
-                const int64_t full = region_items(g, TileRegion{0, g.ntx, ty0, F});
-                const int64_t half = ((yend - F * g.rows + T2 - 1) / T2) * g.ntx;
-                const double t = tail_makespan(full, half, slots);
-                if (t < best - 1e-9) {
-                    best = t;
-                    bq = q;
-                }
-            }
-            if (bq > 0) {
-                a.ty1[0] = ty1 - bq;
-                a.first[1] = region_items(g, TileRegion{0, g.ntx, ty0, a.ty1[0]});
-                a.half_first = a.first[1];
-                a.half_y = a.ty1[0] * g.rows;
-                a.half_yend = yend;
-                a.half_ntx = g.ntx;
-                items = a.half_first + ((yend - a.half_y + T2 - 1) / T2) * g.ntx;
-            }
-        } else if (mode == 1 && slots > 0 && items > slots && rem != 0 && rem <= slots / 2) {
-            int64_t q = 1;
-            while (q < ty1 - ty0 && ((q * g.rows + T2 - 1) / T2) * g.ntx < slots) ++q;
-            if (q < ty1 - ty0) {
-                a.ty1[0] = ty1 - q;
-                a.first[1] = region_items(g, TileRegion{0, g.ntx, ty0, a.ty1[0]});
-                a.half_first = a.first[1];
-                a.half_y = a.ty1[0] * g.rows;
-                a.half_yend = yend;
-                a.half_ntx = g.ntx;
-                items = a.half_first + ((yend - a.half_y + T2 - 1) / T2) * g.ntx;
-            }
+        const int64_t B = g.gsh < 6 ? 64 >> g.gsh : 1;
+        const TailPlan p = tail_plan_for(L, g, m, ty0, ty1);
+        if (p.F < ty1 && p.F >= ty0) {
+            a.ty1[0] = p.F;
+            a.first[1] = region_items(g, TileRegion{0, g.ntx, ty0, p.F});
+            const int64_t y34 = p.F * g.rows, y2 = std::min(y34 + p.n34 * T34, yend);
+            a.sec_first[0] = a.first[1];
+            a.sec_first[1] = a.sec_first[0] + tail_row_items(g.ntx, B, p.n34);
+            a.sec_first[2] = a.sec_first[1] + tail_row_items(g.ntx, B, p.n2);
+            a.sec_y[0] = y34;
+            a.sec_y[1] = y2;
+            a.sec_y[2] = yend;
+            items = a.sec_first[2];
         }
     }
-    a.xcd_n = (bit ? xcd_order_enabled() : xcd_order_byte_enabled()) ? (a.half_first > 0 ? a.half_first : items) : 0;
+    const bool split = a.sec_first[2] > 0;
+    a.xcd_n = (bit ? xcd_order_enabled() : xcd_order_byte_enabled()) ? (split ? a.sec_first[0] : items) : 0;
     if (valu_lane_ops) {
-        *valu_lane_ops = (double)(a.half_first > 0 ? a.half_first : items) * 64.0 * tstep_valu_per_tile_lane(m, !bit);
-        if (a.half_first > 0)  // half tiles: R / 2 register rows per wave
-            *valu_lane_ops += (double)(items - a.half_first) * 64.0 * 0.5 * tstep_valu_per_tile_lane(m, !bit);
+        const double lane = 64.0 * tstep_valu_per_tile_lane(m, !bit);
+        *valu_lane_ops = (double)(split ? a.sec_first[0] : items) * lane;
+        if (split)  // 3/4- and half-height tiles: 3R / 4 and R / 2 register rows per wave
+            *valu_lane_ops += lane * ((double)(a.sec_first[1] - a.sec_first[0]) * (double)(Rb * 3 / 4) / Rb +
+                                      (double)(a.sec_first[2] - a.sec_first[1]) * (double)(Rb / 2) / Rb);
     }
     const void *fn = bit                      ? bit_k(wrap)
                      : byte_one_ghost(L, m) ? byte_fn<48, 1>(wrap)

@@ -143,6 +143,31 @@ def test_single_launch_tail_split(gpu, kernel, nx, ny, gens, bmax):
         assert (life.checksum(), life.live_count()) == got
 
 
+@pytest.mark.parametrize("nx,ny,bmax,gens", [(16384, 32768, 12, 24), (16384, 32768, 10, 20), (16384, 32768, 11, 33),
+                                             (32768, 16384, 12, 36), (65536, 8192, 12, 12)])
+def test_partial_height_tail_tiles_band_vs_oracle(gpu, oracle, nx, ny, bmax, gens):
+    """Round 6: a launch of just over one round of tiles
+    (configs[3]'s N = 8 block, 16384 x 32768: 833 tiles on 768 slots) is
+    re-tiled at the bottom as 3/4- and half-height tiles, banded in the last
+    tile column like the full tiles (LIFE_TAIL_SPLIT 3, life::tail_plan).
+    Pinned to the CPU oracle on a full-height band of 2048 + 2 x 64 columns
+    around the x = 0 seam: it holds the banded last tile column, the x wrap
+    and every partial-height tile row; the band's cut edges are wrong by at
+    most `gens` < 64 cells."""
+    half, margin = 1024, 64
+    band = oracle.fill_random_window(nx, nx - half - margin, 0, 2 * (half + margin), ny, seed=7, density=0.5)
+    cols = np.r_[nx - half:nx, 0:half]
+    with gpu.Life(nx, ny, kernel="bit", flow=0) as life:
+        life.configure(gpu.OPT_BLOCK_GENS, bmax)
+        life.fill_random(7, 0.5)
+        life.set_timing(True)
+        life.step(gens)
+        assert life.last_path() == "tiles"
+        got = life.gather()[:, cols]
+    band = oracle.life_run(band, gens, threads=_threads())
+    np.testing.assert_array_equal(got, band[:, margin:margin + 2 * half])
+
+
 def test_row_strip_interior_tail_split(gpu):
     """The interior launch of a row strip (one full-width region of tile rows
     [ra, rb) while the ring runs concurrently) takes half-height tail tiles
