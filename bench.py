@@ -374,9 +374,14 @@ def main():
     # is timed by its span only (set_timing(3)): per-launch events there put
     # ~10 us between back-to-back launches (profiles/r05/c, d).  Its kernel
     # statistics (the roofline object) and the overlapped schedule's phase
-    # events (the "phases" object) are then recorded after the timed region
-    # and the parity check, over K more generations (one exchange at least:
-    # with the deep halo a short call may hold none).
+    # events (the "phases" object) are then recorded right after the timed
+    # region, over K more generations (one exchange at least: with the deep
+    # halo a short call may hold none), before anything else runs on the GPU:
+    # recorded after the parity run and the copy-ceiling probe instead (round
+    # 5), the same kernels ran 8-10 % faster than inside the timed call (the
+    # GPU back at its idle clock; profiles/r06/a trace_loop96_oneshot: plain
+    # passes 0.494-0.501 ms in the call, 0.454-0.457 ms in the statistics run),
+    # so the phases understated the call's own blocks.
     # LIFE_BENCH_PHASES_TIMED=1 (or no warmup): all of it inside the timed call.
     phases_timed = os.environ.get("LIFE_BENCH_PHASES_TIMED", "0") == "1" or a.warmup <= 0
     multi = n_gpus > 1 or a.loopback
@@ -417,9 +422,14 @@ def main():
     call = life.call_stats()  # host enqueue / device span of the timed call
     elapsed, host_enq, pass_enq, span = allmax([elapsed, call["host_enqueue_ms"], call["pass_enqueue_max_ms"],
                                                 call["device_span_ms"]])
-    if not stats_after:
-        avg_ms, launches, bytes_per_launch = life.kernel_stats()
-        updates_per_launch, valu_per_launch = life.kernel_work()
+    K = life.layout().generations_per_exchange
+    if stats_after:
+        life.set_timing(True)
+        life.step(K)
+        life.sync()
+        ph = life.phase_stats()
+    avg_ms, launches, bytes_per_launch = life.kernel_stats()
+    updates_per_launch, valu_per_launch = life.kernel_work()
     if phases_timed:
         ph = life.phase_stats()
     live = life.live_count()
@@ -432,15 +442,9 @@ def main():
 
     parity = None
     if n_gpus > 1 and not a.no_parity:
-        parity = parity_vs_1gpu(a, life, grid, nx, ny, a.warmup + a.steps, elapsed, n_gpus, rank, dist,
-                                barrier_sync)
-    if stats_after:
-        life.set_timing(True)
-        life.step(lay.generations_per_exchange)
-        life.sync()
-        ph = life.phase_stats()
-        avg_ms, launches, bytes_per_launch = life.kernel_stats()
-        updates_per_launch, valu_per_launch = life.kernel_work()
+        # the grid has advanced warmup + steps (+ K statistics generations)
+        parity = parity_vs_1gpu(a, life, grid, nx, ny, a.warmup + a.steps + (K if stats_after else 0), elapsed,
+                                n_gpus, rank, dist, barrier_sync)
     if multi:
         exposed = allmax([ph["block_ms"] - ph["interior_ms"], ph["block_ms"], ph["halo_ms"]])
 
