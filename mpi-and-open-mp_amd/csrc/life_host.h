@@ -48,30 +48,29 @@ int gather_plan(int64_t nx, int64_t ny, int dims0, int dims1, int kernel, int fm
 
 // Launch-tail plan of one bit-tile launch over a full-width region (tile
 // rows [ty0, ty1) of T owned rows each, the region ending at owned row
-// yend): the first F tile rows stay full tiles, then n34 tile rows of
-// 3/4-height tiles (T34 owned rows) and n2 of half-height tiles (T2), both
-// banded in the last tile column like the full ones, so that the launch's
-// last rounds are short items filling the slots the full tiles leave
-// (life_kernels.hip launch_tstep).  Items of r tile rows:
-// (ntx - 1) r + ceil(r / B) with bands of B tile rows (B > 1), else ntx r.
-// The plan minimises the makespan of a list schedule (items dealt in launch
-// order to the earliest free of `slots` resident workgroups) with item
-// durations 1 (full), c + (1 - c) 3/4 and c + (1 - c) / 2, c the fixed share
-// of a tile (window load, store, turnover).  mode 1: round 4's rule (half
-// tiles for the bottom rows when the last round is under half full), 2: the
-// model with half tiles only, 3: the model with 3/4 and half tiles.  F == ty1:
-// no split.  Plans are cached per argument set (a launch repeats its shape).
+// yend): the first F tile rows stay full tiles, the rest become n2 tile rows
+// of half-height tiles (T2 owned rows), banded in the last tile column like
+// the full ones, dispatched last, so that the launch's last round is short
+// items filling the slots the full tiles leave (life_kernels.hip
+// launch_tstep).  Items of r tile rows: (ntx - 1) r + ceil(r
+// / B) with bands of B tile rows (B > 1), else ntx r.  mode 1: round 4's rule
+// (the fewest bottom rows whose half tiles fill one round, when the last
+// round is under half full); mode 2: the split with the smallest makespan of
+// a list schedule (items dealt in launch order to the earliest free of
+// `slots` resident workgroups; full tiles last 1, half tiles c + (1 - c) /
+// 2, c the fixed share of a tile: window load, stores, turnover).  F == ty1:
+// no split.  Cached per argument set (a launch repeats its shape).
 struct TailPlan {
-    int64_t F = 0, n34 = 0, n2 = 0;
+    int64_t F = 0, n2 = 0;
     double makespan = 0.0;  // model tile-times (full tile = 1)
 };
 // items of `rows` full-width tile rows (banded last column when B > 1)
 inline int64_t tail_row_items(int64_t ntx, int64_t B, int64_t rows) {
     return rows <= 0 ? 0 : B > 1 ? (ntx - 1) * rows + (rows + B - 1) / B : ntx * rows;
 }
-// the list schedule's makespan of F full rows, then n34 and n2 rows
-double tail_makespan3(int64_t ntx, int64_t B, int64_t F_rows, int64_t n34, int64_t n2, int64_t slots, double c);
-TailPlan tail_plan(int64_t ntx, int64_t B, int64_t ty0, int64_t ty1, int64_t yend, int64_t T, int64_t T34, int64_t T2,
+// the list schedule's makespan of F_rows full tile rows, then n2 half rows
+double tail_makespan2(int64_t ntx, int64_t B, int64_t F_rows, int64_t n2, int64_t slots, double c);
+TailPlan tail_plan(int64_t ntx, int64_t B, int64_t ty0, int64_t ty1, int64_t yend, int64_t T, int64_t T2,
                    int64_t slots, int mode, double c);
 
 }  // namespace life

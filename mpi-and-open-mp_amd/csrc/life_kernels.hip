@@ -299,14 +299,11 @@ struct TArgs {
     int32_t gsh;
     int64_t bcol;
     // tail split (bit, one launch of one full-width region; launch_tstep):
-    // workgroups [sec_first[0], sec_first[1]) run 3/4-height tiles (3R / 4
-    // rows per wave) over owned rows [sec_y[0], sec_y[1]), workgroups
-    // [sec_first[1], sec_first[2]) half-height tiles (R / 2 rows per wave)
-    // over rows [sec_y[1], sec_y[2]); each section's tile rows span all ntx
-    // tile columns, the last one banded like the full tiles (gsh < 6).  The
-    // last rounds of a launch are then shorter items that fill the slots the
-    // full tiles leave.  sec_first[2] == 0: no split.
-    int64_t sec_first[3], sec_y[3], sec_ntx;
+    // with tail_ntx > 0, workgroups >= tail_first run half-height tiles (R /
+    // 2 rows per wave) over owned rows [tail_y, tail_yend), tail_ntx tile
+    // columns per tile row, the last one banded like the full tiles (gsh <
+    // 6), so the last round of a launch is made of half-length items
+    int64_t tail_first, tail_y, tail_yend, tail_ntx;
     // XCD-aware order (bit, LIFE_XCD_ORDER): workgroups [0, xcd_n) are
     // renumbered so that each XCD (blocks b, b + 8, ... share one) walks a
     // contiguous row-major run of items; 0: dispatch order
@@ -740,16 +737,18 @@ __device__ __forceinline__ void tile_body_byte(const TArgs &a, const uint8_t *in
 // (R = 16) or 1 at 128.
 constexpr int bit_wpe(int NW, int R) { return NW == 16 ? (R <= 16 ? 8 : 4) : (R <= 24 ? 6 : 4); }
 
-// Item i of a tail section (TArgs::sec_*): RS rows per wave, tile rows of
-// TS = NW RS - 2m owned rows from owned row y0, the last one stopping at
-// yend; ntx - 1 ordinary tiles per tile row, then the banded items of the
-// last tile column (B = 64 >> gsh tile rows each), or ntx tiles per row.
+// Item i of the tail (TArgs::tail_*): RS rows per wave, tile rows of TS =
+// NW RS - 2m owned rows from owned row tail_y, the last one stopping at
+// tail_yend; tail_ntx - 1 ordinary tiles per tile row, then the banded items
+// of the last tile column (B = 64 >> gsh tile rows each), or tail_ntx tiles
+// per row.  (Round 5's half tiles spanned the last column as full-width
+// tiles; banded they take (64 - o - 2) / 64 fewer lanes there.)
 template <int RS, bool WRAPX, bool WRAPY, int NW>
-__device__ __forceinline__ void tail_item(const TArgs &a, int64_t i, int64_t y0, int64_t yend, XchB<NW> &xch) {
-    const int64_t TS = (int64_t)NW * RS - 2 * a.m;
+__device__ __forceinline__ void tail_item(const TArgs &a, int64_t i, XchB<NW> &xch) {
+    const int64_t TS = (int64_t)NW * RS - 2 * a.m, y0 = a.tail_y, yend = a.tail_yend;
     const int64_t rows = (yend - y0 + TS - 1) / TS;
     const bool band = a.gsh < 6;
-    const int64_t ntxs = a.sec_ntx - (band ? 1 : 0), nfull = ntxs * rows;
+    const int64_t ntxs = a.tail_ntx - (band ? 1 : 0), nfull = ntxs * rows;
     if (i < nfull) {
         tile_body_bit<RS, WRAPX, WRAPY, 0, NW>(a, a.in, a.out, i % ntxs, i / ntxs, xch, 6, 1, y0, yend);
     } else {
@@ -773,11 +772,8 @@ __global__ __launch_bounds__(64 * NW, bit_wpe(NW, R)) void tstep_bit_kernel(TArg
         const int64_t n = a.xcd_n, x = wg & 7, k = wg >> 3, per = n >> 3, rem = n & 7;
         wg = (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + k;
     }
-    if (a.sec_first[2] > 0 && wg >= a.sec_first[0]) {
-        if (wg < a.sec_first[1])
-            tail_item<R * 3 / 4, WRAPX, WRAPY, NW>(a, wg - a.sec_first[0], a.sec_y[0], a.sec_y[1], xch);
-        else
-            tail_item<R / 2, WRAPX, WRAPY, NW>(a, wg - a.sec_first[1], a.sec_y[1], a.sec_y[2], xch);
+    if (a.tail_ntx > 0 && wg >= a.tail_first) {
+        tail_item<R / 2, WRAPX, WRAPY, NW>(a, wg - a.tail_first, xch);
         wg_trace(1);
         return;
     }
@@ -1894,17 +1890,17 @@ static bool xcd_order_byte_enabled() {
     return on;
 }
 
-// LIFE_TAIL_SPLIT: 0 no partial-height tail tiles, 1 the round-4 rule (the
+// LIFE_TAIL_SPLIT: 0 no half-height tail tiles, 1 the round-4 rule (the
 // fewest bottom tile rows whose half tiles fill one round, when the last
-// round is under half full), 2 (round 5) the split with half tiles a
-// list-scheduling model of the launch says ends first, 3 (default, round 6)
-// the same model choosing among full, 3/4- and half-height tiles
-// (life::tail_plan, life_plan.cpp; scripts/tail_model.py restates it).
+// round is under half full), 2 (default) the split a list-scheduling model
+// of the launch says ends first (life::tail_plan, life_plan.cpp).  (Round 6
+// measured a third tier, 3/4-height tiles, chosen by the same model: 5-7 %
+// slower at the small blocks, profiles/r06/c -- removed.)
 static int tail_split_mode() {
     static const int v = [] {
         const char *e = getenv("LIFE_TAIL_SPLIT");
-        const int m = e ? atoi(e) : 3;
-        return m >= 0 && m <= 3 ? m : 3;
+        const int m = e ? atoi(e) : 2;
+        return m >= 0 && m <= 2 ? m : 2;
     }();
     return v;
 }
@@ -1968,10 +1964,9 @@ life_layout extended_layout(const life_layout &L, const Extend &ext) {
 // The tail plan of a full-width bit launch over tile rows [ty0, ty1) of
 // tile_geom(L, m) (launch_tstep; cached by life::tail_plan).
 static TailPlan tail_plan_for(const life_layout &L, const TileGeom &g, int m, int64_t ty0, int64_t ty1) {
-    const int Rb = temporal_rows(true), NWb = tile_waves(true), gh = tile_ghost(L, m);
-    const int64_t T34 = (int64_t)NWb * (Rb * 3 / 4) - 2 * gh, T2 = (int64_t)NWb * (Rb / 2) - 2 * gh;
+    const int64_t T2 = (int64_t)tile_waves(true) * (temporal_rows(true) / 2) - 2 * (int64_t)tile_ghost(L, m);
     const int64_t yend = std::min(ty1 * g.rows, L.h), B = g.gsh < 6 ? 64 >> g.gsh : 1;
-    return tail_plan(g.ntx, B, ty0, ty1, yend, g.rows, T34, T2, tstep_bit_slots(), tail_split_mode(), tail_c());
+    return tail_plan(g.ntx, B, ty0, ty1, yend, g.rows, T2, tstep_bit_slots(), tail_split_mode(), tail_c());
 }
 
 void prewarm_tail_plans(const life_layout &L, int mmax, bool ext_y) {
@@ -2027,46 +2022,39 @@ hipError_t launch_tstep(const life_layout &Lin, const uint8_t *in, uint8_t *out,
     }
     if (a.nreg == 0 || m <= 0) return hipSuccess;
     int64_t items = a.first[a.nreg];  // one workgroup per tile (or banded item)
-    for (int k = 0; k < 3; k++) a.sec_first[k] = a.sec_y[k] = 0;
-    a.sec_ntx = g.ntx;
-    const int Rb = temporal_rows(bit), NWb = tile_waves(bit), gh = tile_ghost(L, m);
-    const int64_t T34 = (int64_t)NWb * (Rb * 3 / 4) - 2 * gh, T2 = (int64_t)NWb * (Rb / 2) - 2 * gh;
+    a.tail_first = a.tail_y = a.tail_yend = a.tail_ntx = 0;
+    const int64_t T2 = (int64_t)tile_waves(bit) * (temporal_rows(bit) / 2) - 2 * (int64_t)tile_ghost(L, m);
     if (bit && T2 >= 1 && a.nreg == 1 && a.tx0[0] == 0 && a.tx1[0] == g.ntx && tail_split_mode() > 0) {
         // One full-width region: the whole shard, a deep-halo pass over the
         // extended shard, or the interior of a row strip (the ring runs
         // concurrently).  The launch runs items / slots rounds of equal
         // tiles; a last round under full leaves CUs idle for up to a whole
-        // tile time.  The bottom tile rows are re-tiled as 3/4- and
-        // half-height tiles, banded in the last column like the full tiles,
-        // dispatched last, so the final rounds are short items filling the
-        // idle slots (life::tail_plan; LIFE_TAIL_SPLIT 3, round 6; 2: half
-        // tiles only, round 5; 1: round 4's rule; 0: off).  The byte tiles
-        // (2 per CU, 32 ghost rows: a third of a half tile) lost 3-4 % with
-        // half tiles (profiles/r02/r2z) and keep whole tiles.
+        // tile time.  The bottom tile rows are re-tiled as half-height tiles
+        // (banded in the last column like the full tiles, round 6),
+        // dispatched last, so the final round is half-length items on every
+        // slot (life::tail_plan).  The byte tiles (2 per CU, 32 ghost rows: a
+        // third of a half tile) lost 3-4 % with half tiles (profiles/r02/r2z)
+        // and keep whole tiles.
         const int64_t ty0 = a.ty0[0], ty1 = a.ty1[0], yend = std::min(ty1 * g.rows, L.h);
         const int64_t B = g.gsh < 6 ? 64 >> g.gsh : 1;
         const TailPlan p = tail_plan_for(L, g, m, ty0, ty1);
         if (p.F < ty1 && p.F >= ty0) {
             a.ty1[0] = p.F;
             a.first[1] = region_items(g, TileRegion{0, g.ntx, ty0, p.F});
-            const int64_t y34 = p.F * g.rows, y2 = std::min(y34 + p.n34 * T34, yend);
-            a.sec_first[0] = a.first[1];
-            a.sec_first[1] = a.sec_first[0] + tail_row_items(g.ntx, B, p.n34);
-            a.sec_first[2] = a.sec_first[1] + tail_row_items(g.ntx, B, p.n2);
-            a.sec_y[0] = y34;
-            a.sec_y[1] = y2;
-            a.sec_y[2] = yend;
-            items = a.sec_first[2];
+            a.tail_first = a.first[1];
+            a.tail_y = p.F * g.rows;
+            a.tail_yend = yend;
+            a.tail_ntx = g.ntx;
+            items = a.tail_first + tail_row_items(g.ntx, B, p.n2);
         }
     }
-    const bool split = a.sec_first[2] > 0;
-    a.xcd_n = (bit ? xcd_order_enabled() : xcd_order_byte_enabled()) ? (split ? a.sec_first[0] : items) : 0;
+    const bool split = a.tail_ntx > 0;
+    a.xcd_n = (bit ? xcd_order_enabled() : xcd_order_byte_enabled()) ? (split ? a.tail_first : items) : 0;
     if (valu_lane_ops) {
         const double lane = 64.0 * tstep_valu_per_tile_lane(m, !bit);
-        *valu_lane_ops = (double)(split ? a.sec_first[0] : items) * lane;
-        if (split)  // 3/4- and half-height tiles: 3R / 4 and R / 2 register rows per wave
-            *valu_lane_ops += lane * ((double)(a.sec_first[1] - a.sec_first[0]) * (double)(Rb * 3 / 4) / Rb +
-                                      (double)(a.sec_first[2] - a.sec_first[1]) * (double)(Rb / 2) / Rb);
+        *valu_lane_ops = (double)(split ? a.tail_first : items) * lane;
+        if (split)  // half tiles: R / 2 register rows per wave
+            *valu_lane_ops += (double)(items - a.tail_first) * lane * 0.5;
     }
     const void *fn = bit                      ? bit_k(wrap)
                      : byte_one_ghost(L, m) ? byte_fn<48, 1>(wrap)

@@ -346,100 +346,72 @@ struct SlotGroups {
 };
 
 struct TailKey {
-    int64_t ntx, B, ty0, ty1, yend, T, T34, T2, slots;
+    int64_t ntx, B, ty0, ty1, yend, T, T2, slots;
     int mode;
     double c;
     bool operator==(const TailKey &o) const {
-        return ntx == o.ntx && B == o.B && ty0 == o.ty0 && ty1 == o.ty1 && yend == o.yend && T == o.T && T34 == o.T34 &&
-               T2 == o.T2 && slots == o.slots && mode == o.mode && c == o.c;
+        return ntx == o.ntx && B == o.B && ty0 == o.ty0 && ty1 == o.ty1 && yend == o.yend && T == o.T && T2 == o.T2 &&
+               slots == o.slots && mode == o.mode && c == o.c;
     }
 };
 }  // namespace
 
-double life::tail_makespan3(int64_t ntx, int64_t B, int64_t F_rows, int64_t n34, int64_t n2, int64_t slots,
-                            double c) {
+double life::tail_makespan2(int64_t ntx, int64_t B, int64_t F_rows, int64_t n2, int64_t slots, double c) {
     if (slots < 1) return 0.0;
     const int64_t nf = tail_row_items(ntx, B, F_rows);
     const int64_t r = nf / slots, rem = nf % slots;
     SlotGroups g;
     g.add((double)r, slots - rem);
     if (rem) g.add((double)(r + 1), rem);
-    double end = nf ? (double)(r + (rem ? 1 : 0)) : 0.0;
-    end = g.deal(c + (1.0 - c) * 0.75, tail_row_items(ntx, B, n34), end);
+    const double end = nf ? (double)(r + (rem ? 1 : 0)) : 0.0;
     return g.deal(c + (1.0 - c) * 0.5, tail_row_items(ntx, B, n2), end);
 }
 
 life::TailPlan life::tail_plan(int64_t ntx, int64_t B, int64_t ty0, int64_t ty1, int64_t yend, int64_t T,
-                               int64_t T34, int64_t T2, int64_t slots, int mode, double c) {
+                               int64_t T2, int64_t slots, int mode, double c) {
     TailPlan none;
     none.F = ty1;
-    if (ntx < 1 || ty1 <= ty0 || T < 1 || T2 < 1 || slots < 1 || mode < 1 || mode > 3) return none;
-    if (mode == 3 && T34 < 1) mode = 2;
+    if (ntx < 1 || ty1 <= ty0 || T < 1 || T2 < 1 || slots < 1 || mode < 1 || mode > 2) return none;
     const int64_t nall = tail_row_items(ntx, B, ty1 - ty0);
-    none.makespan = tail_makespan3(ntx, B, ty1 - ty0, 0, 0, slots, c);
+    none.makespan = tail_makespan2(ntx, B, ty1 - ty0, 0, slots, c);
     // Whole rounds: nothing to fill.  One round or less: the model's slots are
     // not independent there (a CU's three slots share its SIMDs, and a lone
     // tile runs faster), so it is not trusted to re-tile an underfilled launch.
     if (nall <= slots || nall % slots == 0) return none;
     static std::mutex mu;
     static std::vector<std::pair<TailKey, TailPlan>> cache;
-    const TailKey key{ntx, B, ty0, ty1, yend, T, T34, T2, slots, mode, c};
+    const TailKey key{ntx, B, ty0, ty1, yend, T, T2, slots, mode, c};
     {
         std::lock_guard<std::mutex> lk(mu);
         for (const auto &e : cache)
             if (e.first == key) return e.second;
     }
     TailPlan best = none;
-    // rows the partial tiles of (F, n34) leave to the half tiles
-    auto halves = [&](int64_t F, int64_t n34) -> int64_t {
-        const int64_t left = yend - F * T - n34 * T34;
+    auto halves = [&](int64_t F) -> int64_t {
+        const int64_t left = yend - F * T;
         return left > 0 ? (left + T2 - 1) / T2 : 0;
-    };
-    auto consider = [&](int64_t F, int64_t n34) {
-        const int64_t rest = yend - F * T;
-        if (rest <= 0 || n34 < 0 || (n34 > 0 && (n34 - 1) * T34 >= rest)) return;  // over-covering
-        const int64_t n2 = halves(F, n34);
-        const double t = tail_makespan3(ntx, B, F - ty0, n34, n2, slots, c);
-        if (t < best.makespan - 1e-9) {
-            best.F = F;
-            best.n34 = n34;
-            best.n2 = n2;
-            best.makespan = t;
-        }
     };
     if (mode == 1) {
         // round 4's rule: the fewest bottom rows whose half tiles fill one
         // round, when the last round is under half full
-        const int64_t rem = nall % slots;
-        if (rem <= slots / 2) {
+        if (nall % slots <= slots / 2) {
             int64_t q = 1;
             while (q < ty1 - ty0 && tail_row_items(ntx, B, (q * T + T2 - 1) / T2) < slots) ++q;
             if (q < ty1 - ty0) {
                 best.F = ty1 - q;
-                best.n34 = 0;
-                best.n2 = halves(best.F, 0);
-                best.makespan = tail_makespan3(ntx, B, best.F - ty0, 0, best.n2, slots, c);
+                best.n2 = halves(best.F);
+                best.makespan = tail_makespan2(ntx, B, best.F - ty0, best.n2, slots, c);
             }
         }
     } else {
-        // partial tiles for at most ~1.5 rounds of full items' worth of rows
-        const int64_t per_row = tail_row_items(ntx, B, 64) / 64 + 1;
-        const int64_t qmax = std::min<int64_t>(ty1 - ty0, (3 * slots) / (2 * per_row) + 2);
-        const int64_t Flo = ty1 - qmax;
-        if (mode == 2) {
-            for (int64_t F = ty1 - 1; F >= Flo; --F) consider(F, 0);
-        } else {
-            // coarse grid, then every point around the best of it
-            auto n34max = [&](int64_t F) { return (yend - F * T + T34 - 1) / T34; };
-            const int64_t sF = std::max<int64_t>(1, qmax / 24), s34 = std::max<int64_t>(1, n34max(Flo) / 24);
-            for (int64_t F = ty1 - 1; F >= Flo; F -= sF)
-                for (int64_t n = 0; n <= n34max(F); n += s34) consider(F, n);
-            if (sF > 1 || s34 > 1) {
-                const TailPlan c0 = best;
-                const int64_t F0 = c0.F == ty1 ? ty1 - 1 : c0.F, n0 = c0.n34;
-                for (int64_t F = std::min(ty1 - 1, F0 + sF); F >= std::max(Flo, F0 - sF); --F)
-                    for (int64_t n = std::max<int64_t>(0, n0 - s34); n <= std::min(n34max(F), n0 + s34); ++n)
-                        consider(F, n);
+        // every split point (ties keep more full tiles)
+        for (int64_t F = ty1 - 1; F >= ty0; --F) {
+            const int64_t n2 = halves(F);
+            const double t = tail_makespan2(ntx, B, F - ty0, n2, slots, c);
+            if (t < best.makespan - 1e-9) {
+                best.F = F;
+                best.n2 = n2;
+                best.makespan = t;
             }
         }
     }

@@ -145,11 +145,11 @@ def test_single_launch_tail_split(gpu, kernel, nx, ny, gens, bmax):
 
 @pytest.mark.parametrize("nx,ny,bmax,gens", [(16384, 32768, 12, 24), (16384, 32768, 10, 20), (16384, 32768, 11, 33),
                                              (32768, 16384, 12, 36), (65536, 8192, 12, 12)])
-def test_partial_height_tail_tiles_band_vs_oracle(gpu, oracle, nx, ny, bmax, gens):
+def test_banded_half_tail_tiles_band_vs_oracle(gpu, oracle, nx, ny, bmax, gens):
     """Round 6: a launch of just over one round of tiles
     (configs[3]'s N = 8 block, 16384 x 32768: 833 tiles on 768 slots) is
-    re-tiled at the bottom as 3/4- and half-height tiles, banded in the last
-    tile column like the full tiles (LIFE_TAIL_SPLIT 3, life::tail_plan).
+    re-tiled at the bottom as half-height tiles, banded in the last tile
+    column like the full tiles (life::tail_plan).
     Pinned to the CPU oracle on a full-height band of 2048 + 2 x 64 columns
     around the x = 0 seam: it holds the banded last tile column, the x wrap
     and every partial-height tile row; the band's cut edges are wrong by at

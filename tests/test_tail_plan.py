@@ -1,17 +1,15 @@
 """The launch-tail planner (life::tail_plan, csrc/life_plan.cpp; CPU only).
 
 launch_tstep re-tiles the bottom tile rows of a full-width bit launch as
-3/4- and half-height tiles (banded in the last tile column like the full
-tiles) so that the launch's last rounds are short items filling the slots
-the full tiles leave (configs[3]'s N = 8
-block, 833 tiles on 768 slots, runs ~1.5 tile-times per pass with half tiles
-only).  Checked here with a g++ harness against a Python heap simulation of
-the same list schedule:
+half-height tiles, banded in the last tile column like the full tiles (round
+6), so that the launch's last round is short items filling the slots the
+full tiles leave.  Checked here with a g++ harness against a
+Python heap simulation of the same list schedule:
 
-* tail_makespan3 (grouped slots) == the heap simulation for every count;
+* tail_makespan2 (grouped slots) == the heap simulation for every count;
 * the plan's own makespan is the simulated makespan of its split, it covers
-  the region's rows exactly once, never loses to no split or to half tiles
-  only, and is within 2 % of the exhaustive optimum over (F, n34).
+  the region's rows exactly once, never loses to no split, and is the
+  optimum over every split point; round 4's rule (mode 1) is never better.
 """
 import heapq
 import os
@@ -28,33 +26,16 @@ HARNESS = r"""
 #include <string.h>
 #include "life_host.h"
 int main(int argc, char **argv) {
-    if (!strcmp(argv[1], "span")) {  // ntx B F n34 n2 slots c
-        printf("%.9f\n", life::tail_makespan3(atoll(argv[2]), atoll(argv[3]), atoll(argv[4]), atoll(argv[5]),
-                                              atoll(argv[6]), atoll(argv[7]), atof(argv[8])));
+    if (!strcmp(argv[1], "span")) {  // ntx B F n2 slots c
+        printf("%.9f\n", life::tail_makespan2(atoll(argv[2]), atoll(argv[3]), atoll(argv[4]), atoll(argv[5]),
+                                              atoll(argv[6]), atof(argv[7])));
         return 0;
     }
-    if (!strcmp(argv[1], "best")) {  // exhaustive optimum over (F, n34): ntx B nty h T T34 T2 slots c
-        const long long ntx = atoll(argv[2]), B = atoll(argv[3]), nty = atoll(argv[4]), h = atoll(argv[5]),
-                        T = atoll(argv[6]), T34 = atoll(argv[7]), T2 = atoll(argv[8]), slots = atoll(argv[9]);
-        const double c = atof(argv[10]);
-        double best = life::tail_makespan3(ntx, B, nty, 0, 0, slots, c);
-        for (long long f = nty - 1; f >= 0; --f) {
-            const long long rest = h - f * T;
-            for (long long n = 0; n <= (rest + T34 - 1) / T34; ++n) {
-                if (n && (n - 1) * T34 >= rest) continue;
-                const long long k = rest > n * T34 ? (rest - n * T34 + T2 - 1) / T2 : 0;
-                const double t = life::tail_makespan3(ntx, B, f, n, k, slots, c);
-                if (t < best) best = t;
-            }
-        }
-        printf("%.9f\n", best);
-        return 0;
-    }
-    long long v[9];
-    for (int i = 0; i < 9; i++) v[i] = atoll(argv[2 + i]);
-    const life::TailPlan p = life::tail_plan(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8], atoi(argv[11]),
-                                             atof(argv[12]));
-    printf("%lld %lld %lld %.9f\n", (long long)p.F, (long long)p.n34, (long long)p.n2, p.makespan);
+    long long v[8];
+    for (int i = 0; i < 8; i++) v[i] = atoll(argv[2 + i]);
+    const life::TailPlan p = life::tail_plan(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], atoi(argv[10]),
+                                             atof(argv[11]));
+    printf("%lld %lld %.9f\n", (long long)p.F, (long long)p.n2, p.makespan);
     return 0;
 }
 """
@@ -78,10 +59,9 @@ def row_items(ntx, B, rows):
     return 0 if rows <= 0 else ((ntx - 1) * rows + -(-rows // B) if B > 1 else ntx * rows)
 
 
-def heap_span(ntx, B, F, n34, n2, slots, c):
+def heap_span(ntx, B, F, n2, slots, c):
     free, end = [0.0] * slots, 0.0
-    for d, n in ((1.0, row_items(ntx, B, F)), (c + (1 - c) * 0.75, row_items(ntx, B, n34)),
-                 (c + (1 - c) * 0.5, row_items(ntx, B, n2))):
+    for d, n in ((1.0, row_items(ntx, B, F)), (c + (1 - c) * 0.5, row_items(ntx, B, n2))):
         for _ in range(n):
             t = heapq.heappop(free) + d
             end = max(end, t)
@@ -90,59 +70,62 @@ def heap_span(ntx, B, F, n34, n2, slots, c):
 
 
 def geometry(W, m, R=24, NW=8):
-    """tile_geom's columns / bands of a W-pair-wide shard and the three tile heights at m generations"""
+    """tile_geom's columns / bands of a W-pair-wide shard and the full / half tile heights at m generations"""
     ntx = -(-W // 62)
     o = W - 62 * (ntx - 1)
     gsh = 2
     while (1 << gsh) < o + 2:
         gsh += 1
     B = 64 >> gsh if gsh <= 5 else 1
-    return ntx, B, NW * R - 2 * m, NW * (R * 3 // 4) - 2 * m, NW * (R // 2) - 2 * m
+    return ntx, B, NW * R - 2 * m, NW * (R // 2) - 2 * m
 
 
-@pytest.mark.parametrize("ntx,B,F,n34,n2,slots", [(5, 4, 7, 3, 2, 13), (17, 1, 30, 0, 4, 64), (9, 2, 0, 12, 11, 8),
-                                                   (3, 16, 40, 9, 0, 3), (1, 1, 5, 5, 5, 1), (5, 4, 196, 0, 0, 768)])
+@pytest.mark.parametrize("ntx,B,F,n2,slots", [(5, 4, 7, 2, 13), (17, 1, 30, 4, 64), (9, 2, 0, 11, 8), (3, 16, 40, 0, 3),
+                                              (1, 1, 5, 5, 1), (5, 4, 196, 0, 768), (5, 4, 180, 36, 768)])
 @pytest.mark.parametrize("c", [0.0, 0.06, 0.2])
-def test_grouped_schedule_is_the_list_schedule(exe, ntx, B, F, n34, n2, slots, c):
-    got = float(run(exe, "span", ntx, B, F, n34, n2, slots, c)[0])
-    assert got == pytest.approx(heap_span(ntx, B, F, n34, n2, slots, c), abs=1e-9)
+def test_grouped_schedule_is_the_list_schedule(exe, ntx, B, F, n2, slots, c):
+    got = float(run(exe, "span", ntx, B, F, n2, slots, c)[0])
+    assert got == pytest.approx(heap_span(ntx, B, F, n2, slots, c), abs=1e-9)
 
 
 SHAPES = [(1024, 65536), (512, 65536), (512, 32768), (256, 32768), (256, 8192), (300, 5000), (64, 4096), (200, 5000),
-          (300, 2600), (1024, 16384), (700, 9000), (130, 40000)]
+          (1024, 16384), (700, 9000), (130, 40000)]
 
 
 @pytest.mark.parametrize("W,h", SHAPES)
 @pytest.mark.parametrize("m", [5, 10, 12])
-def test_plan_covers_and_beats_the_alternatives(exe, W, h, m):
+def test_plan_covers_and_is_optimal(exe, W, h, m):
     slots, c = 768, 0.06
-    ntx, B, T, T34, T2 = geometry(W, m)
+    ntx, B, T, T2 = geometry(W, m)
     nty = -(-h // T)
-    F, n34, n2, span = run(exe, "plan", ntx, B, 0, nty, h, T, T34, T2, slots, 3, c)
-    F, n34, n2, span = int(F), int(n34), int(n2), float(span)
+    F, n2, span = run(exe, "plan", ntx, B, 0, nty, h, T, T2, slots, 2, c)
+    F, n2, span = int(F), int(n2), float(span)
     assert 0 <= F <= nty
-    if F < nty:  # the split covers rows [F T, h) exactly: no partial row beyond the region
+    if F < nty:  # the half tiles cover rows [F T, h) exactly: no half row beyond the region
         rest = h - F * T
-        assert n34 * T34 + n2 * T2 >= rest
-        assert (n2 == 0 and (n34 - 1) * T34 < rest) or (n2 > 0 and n34 * T34 < rest and (n2 - 1) * T2 < rest - n34 * T34)
+        assert n2 * T2 >= rest > (n2 - 1) * T2
     else:
-        assert n34 == n2 == 0
-    assert span == pytest.approx(heap_span(ntx, B, F, n34, n2, slots, c), abs=1e-9)
-    whole = heap_span(ntx, B, nty, 0, 0, slots, c)
-    half = float(run(exe, "plan", ntx, B, 0, nty, h, T, T34, T2, slots, 2, c)[3])
-    assert span <= whole + 1e-9 and span <= half + 1e-9
-    # exhaustive optimum of the same model over (F, n34) (grouped schedule, exact)
-    if row_items(ntx, B, nty) > slots:  # (an underfilled launch is left whole)
-        best = float(run(exe, "best", ntx, B, nty, h, T, T34, T2, slots, c)[0])
-        assert span <= best * 1.02 + 1e-9, (span, best)
+        assert n2 == 0
+    assert span == pytest.approx(heap_span(ntx, B, F, n2, slots, c), abs=1e-9)
+    whole = heap_span(ntx, B, nty, 0, slots, c)
+    assert span <= whole + 1e-9
+    if row_items(ntx, B, nty) > slots and row_items(ntx, B, nty) % slots:  # (an underfilled launch is left whole)
+        best = min(float(run(exe, "span", ntx, B, f, -(-(h - f * T) // T2), slots, c)[0]) for f in range(nty))
+        assert span <= min(best, whole) + 1e-9
+        rule = float(run(exe, "plan", ntx, B, 0, nty, h, T, T2, slots, 1, c)[2])
+        assert span <= rule + 1e-9
 
 
 def test_known_shapes(exe):
-    """configs[3]'s N = 8 block (16384 x 32768, 256 pairs) at 12 generations per
-    pass: 1.53 tile-times with half tiles only, 1.295 with 3/4 + half tiles;
-    65536^2 at 12: 9.0 (no split helps with half tiles) -> 8.765."""
-    for W, h, m, two, three in [(256, 32768, 12, 1.53, 1.295), (1024, 65536, 12, 9.0, 8.765)]:
-        ntx, B, T, T34, T2 = geometry(W, m)
+    """configs[3]'s N = 8 block (16384 x 32768, 256 pairs, 833 tiles on 768
+    slots) at 12 generations per pass: the full tiles fill one round and the
+    bottom 36 tile rows run as banded half tiles (153 items): 1.53 tile-times
+    instead of 2; 65536^2 at m = 10 (the driver's passes): 8.59 instead of
+    9."""
+    for W, h, m, want, F in [(256, 32768, 12, 1.53, 180), (1024, 65536, 10, 8.59, None)]:
+        ntx, B, T, T2 = geometry(W, m)
         nty = -(-h // T)
-        assert float(run(exe, "plan", ntx, B, 0, nty, h, T, T34, T2, 768, 2, 0.06)[3]) == pytest.approx(two)
-        assert float(run(exe, "plan", ntx, B, 0, nty, h, T, T34, T2, 768, 3, 0.06)[3]) == pytest.approx(three)
+        f, n2, span = run(exe, "plan", ntx, B, 0, nty, h, T, T2, 768, 2, 0.06)
+        assert float(span) == pytest.approx(want, abs=0.011)
+        if F is not None:
+            assert int(f) == F
