@@ -213,6 +213,29 @@ def test_driver_shape_65536_band_vs_oracle(gpu, oracle):
             np.testing.assert_array_equal(got, band[:, margin:margin + 2 * half], err_msg=f"after +{gens}")
 
 
+@pytest.mark.timeout(600)
+def test_driver_shape_65536_whole_grid_vs_oracle(gpu, oracle):
+    """The headline configuration pinned to the CPU oracle on EVERY cell
+    (What's weak 1: the 65536^2 checks were a 2048-column band
+    against the oracle plus N LOCAL shards against one HIP shard): 65536^2,
+    seed 1, the driver's 5-generation then 20-generation calls (per-launch
+    tiles with the banded half-height tail, flow 0), the whole 4 Gcell grid
+    gathered after each call and compared with the OpenMP oracle stepped
+    from the same generator (~107 G cell-updates on the host's cores, 8.6 GB
+    of host arrays)."""
+    n = 65536
+    g = oracle.fill_random(n, n, 1, 0.5)
+    with gpu.Life(n, n, kernel="bit", flow=0) as life:
+        life.fill_random(1, 0.5)
+        for gens in (5, 20):
+            life.step(gens)
+            assert life.last_path() == "tiles"
+            got = life.gather()
+            g = oracle.life_run(g, gens, threads=_threads())
+            assert np.array_equal(got, g), f"after +{gens}: {int(np.count_nonzero(got != g))} cells differ"
+            del got
+
+
 @pytest.mark.timeout(420)
 def test_c3_1000_generations_band_vs_oracle(gpu, oracle):
     """configs[2] at its stated length: random 50 %
