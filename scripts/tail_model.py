@@ -11,6 +11,13 @@ simulation -- the 32768^2 pass is 2.17 ideal, 2.5 at best, which is why
 geometry alone does not fix the small shapes.
 
     python3 scripts/tail_model.py [slots]
+
+Round 6: the product's planner is life::tail_plan (csrc/life_plan.cpp): the
+same list schedule simulated over slot groups, half tiles banded in the last
+tile column like the full ones and lasting c + (1 - c) / 2 of a full tile
+(c = 0.06), checked against a heap simulation and an exhaustive search by
+tests/test_tail_plan.py.  This script keeps round 5's closed form (unbanded
+half tiles of exactly half the duration) for the comparison.
 """
 import heapq
 import sys
