@@ -1249,9 +1249,16 @@ static int flow_form(const life_dev *d, int *m_out) {
     // automatic: the dataflow form (write-through hand-off) when a pass is
     // under kFlowAutoRounds rounds of resident workgroups -- 32768^2 (2.2
     // rounds of 768) +8 %, 32768 x 65536 (4.3) +1 %, 65536^2 (8.6) -3 %
-    // (profiles/r05/a)
-    if (d->flow == 3)
-        return (double)life::flow_items_per_pass(L, m) < kFlowAutoRounds * (double)life::flow_slots(L) ? 1 : 0;
+    // (profiles/r05/a) -- except a pass of 1 to 1.5 rounds: it runs as one
+    // full round plus the banded half-height tail (launch_tstep), its tiles
+    // all finish together and the dataflow form has nothing to pipeline
+    // (16384 x 32768, 833 tiles on 768 slots: per-launch tiles 83.2-83.8 T
+    // against 73.7-75.2 T, profiles/r06/d; under one round the dataflow
+    // form overlaps the passes in the idle slots)
+    if (d->flow == 3) {
+        const double rounds = (double)life::flow_items_per_pass(L, m) / (double)std::max(life::flow_slots(L), 1);
+        return rounds < kFlowAutoRounds && !(rounds >= 1.0 && rounds < 1.5) ? 1 : 0;
+    }
     return d->flow;
 }
 

@@ -108,13 +108,20 @@ def test_flow_needs_four_passes(gpu, oracle):
 def test_flow_default_automatic(gpu):
     """The default (LIFE_OPT_FLOW 3) takes the dataflow form when a pass is
     under 5 rounds of resident workgroups -- the per-launch tiles' tail then
-    idles the chip (32768^2: 2.2 rounds, +8 %, profiles/r05/a) -- and the
-    per-launch tiles at 65536^2 (8.6 rounds, where they win by 3 %)."""
+    idles the chip (32768^2: 2.2 rounds, +8 %, profiles/r05/a) -- except 1 to
+    1.5 rounds, and the per-launch tiles at 65536^2 (8.6 rounds, where they
+    win by 3 %)."""
     with gpu.Life(2048, 1000, kernel="bit", small_grid=False) as life:
         life.fill_random(3, 0.5)
         life.step(100)
         assert life.last_path() == "flow"
     with gpu.Life(65536, 65536, kernel="bit") as life:
+        life.fill_random(3, 0.5)
+        life.step(48)
+        assert life.last_path() == "tiles"
+    # round 6: a pass of 1 to 1.5 rounds (configs[3]'s N = 8 block, 833 tiles)
+    # runs per-launch tiles with the banded half-height tail (+12 %, r06d)
+    with gpu.Life(16384, 32768, kernel="bit") as life:
         life.fill_random(3, 0.5)
         life.step(48)
         assert life.last_path() == "tiles"
