@@ -89,7 +89,7 @@ def parse():
                    help="shard shape (life_dims_choose); default: cart (MPI_Dims_create, life_cart.c:117-118: "
                         "configs[3]'s and configs[4]'s 2-D split); auto = row strips when each is >= 1024 rows tall")
     p.add_argument("--seed", type=int, default=1)
-    p.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline sample budget")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="cpu_baseline sample budget (seconds of CPU work)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--parity-seconds", type=float, default=60.0,
                    help="N > 1: the 1-GPU reference re-runs the timed generations when that is estimated to take "
@@ -133,13 +133,17 @@ def cpu_baseline(target_s: float):
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     n = 4096
     g = O.fill_random(n, n, 12345, 0.5)
-    t = time.perf_counter()
-    g = O.life_run(g, 1, threads)
-    one = max(time.perf_counter() - t, 1e-6)
-    gens = max(1, int(target_s / one))
-    t = time.perf_counter()
-    O.life_run(g, gens, threads)
-    dt = time.perf_counter() - t
+    g = O.life_run(g, 1, threads)  # thread start-up and first touch, untimed
+    # timed: doubling chunks of generations until the budget is spent (a
+    # rate calibrated on a few generations was 3x off)
+    gens, dt, chunk = 0, 0.0, 8
+    while dt < target_s:
+        t = time.perf_counter()
+        g = O.life_run(g, chunk, threads)
+        dt += time.perf_counter() - t
+        gens += chunk
+        per_gen = dt / gens
+        chunk = max(1, min(2 * chunk, int((target_s - dt) / per_gen) + 1))
     return {"value": n * n * gens / dt / 1e9, "unit": "Gcell-updates/s", "cores": threads, "kind": "port",
             "sample": f"random 50% {n}x{n}, {gens} generations, oracle/life_oracle.c OpenMP row strips "
                       f"({threads} threads), {dt:.1f} s",
