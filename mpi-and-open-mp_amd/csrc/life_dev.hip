@@ -610,7 +610,7 @@ bool temporal(const life_dev *d) { return d->shards[0].lay.generations_per_excha
 // Launches up to 4 tile regions of the temporal stencil as ONE kernel on
 // `st` (m generations, cur -> nxt), optionally timed.
 int launch_tiles(life_dev *d, Shard &s, const life::TileRegion *r, int nreg, int m, bool timed, hipStream_t st,
-                 life::Extend ext_ = life::Extend{}) {
+                 life::Extend ext_ = life::Extend{}, int64_t concurrent = 0) {
     const uint8_t *in = s.buf[s.cur];
     uint8_t *out = s.buf[s.cur ^ 1];
     TimedLaunch *t = nullptr;
@@ -624,7 +624,7 @@ int launch_tiles(life_dev *d, Shard &s, const life::TileRegion *r, int nreg, int
     const bool ext = ev && (kEnvTimingMode == kTimeExt || kEnvTimingMode == kTimeCall);
     if (ev && !ext) HIPCHK(hipEventRecord(t->a, st));
     HIPCHK(life::launch_tstep(s.lay, in, out, r, nreg, m, wrap_of(d), st, &valu, ext ? t->a : nullptr,
-                              ext ? t->b : nullptr, xt));
+                              ext ? t->b : nullptr, xt, concurrent));
     if (ev && !ext) HIPCHK(hipEventRecord(t->b, st));
     if (d->timing && timed && t) {  // (no timer counts it -- span-only timing, LIFE_TIMING_MODE=3: no booking)
         const life::TileGeom g = life::tile_geom(life::extended_layout(s.lay, xt), m);
@@ -645,6 +645,18 @@ int launch_tiles(life_dev *d, Shard &s, const life::TileRegion *r, int nreg, int
         d->acc_valu += valu;  // as tiled: tiles, banded items, half-height tail tiles
     }
     return LIFE_OK;
+}
+
+// LIFE_INTERIOR_TAIL (0/1, default 1, read once; A/B knob): the exchange
+// pass's interior launch takes the banded half-height tail, planned with the
+// ring's tiles counted as holding their slots (round 6); 0: no tail split
+// for it (round 5).
+static bool interior_tail() {
+    static const bool v = [] {
+        const char *e = getenv("LIFE_INTERIOR_TAIL");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return v;
 }
 
 // The overlapped schedule of one exchange block (round 5, profiles/r05/c-d
@@ -828,11 +840,16 @@ int generation_block(life_dev *d, int m, bool last) {
         CHK(launch(ring, n, false, s.stream));
         CHK(phase_ring(s, pe[si]));
         const life::TileRegion inner{ca, cb, ra, rb};
-        int64_t items = life::region_items(g, inner);
-        for (int k = 0; k < n; k++) items += life::region_items(g, ring[k]);
+        int64_t ring_items = 0;
+        for (int k = 0; k < n; k++) ring_items += life::region_items(g, ring[k]);
+        const int64_t items = life::region_items(g, inner) + ring_items;
         halo_side[si] = carry_on_halo_side(items, life::tile_slots(s.lay)) ? 1 : 0;
         if (pe[si]) HIPCHK(hipEventRecord(pe[si]->int0, s.stream2));
-        if (rb > ra && cb > ca) CHK(launch(&inner, 1, true, s.stream2));
+        // the interior's launch-tail plan counts the ring's tiles, dispatched
+        // just before it, as holding their slots (round 6: 16384 x 32768's 584
+        // interior tiles beside 249 ring tiles are one round plus a tail)
+        if (rb > ra && cb > ca)
+            CHK(launch_tiles(d, s, &inner, 1, m, true, s.stream2, life::Extend{}, interior_tail() ? ring_items : -1));
         if (pe[si]) HIPCHK(hipEventRecord(pe[si]->int1, s.stream2));
     }
     if (!(rx || ry)) {

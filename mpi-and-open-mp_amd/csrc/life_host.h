@@ -64,13 +64,16 @@ struct TailPlan {
     int64_t F = 0, n2 = 0;
     double makespan = 0.0;  // model tile-times (full tile = 1)
 };
-// items of `rows` full-width tile rows (banded last column when B > 1)
+// items of `rows` tile rows `ntx` tile columns wide (the last column banded
+// in items of B tile rows when B > 1)
 inline int64_t tail_row_items(int64_t ntx, int64_t B, int64_t rows) {
     return rows <= 0 ? 0 : B > 1 ? (ntx - 1) * rows + (rows + B - 1) / B : ntx * rows;
 }
-// the list schedule's makespan of F_rows full tile rows, then n2 half rows
-double tail_makespan2(int64_t ntx, int64_t B, int64_t F_rows, int64_t n2, int64_t slots, double c);
+// the list schedule's makespan of `pre` full items of another launch
+// dispatched first (the ring beside an interior), F_rows full tile rows, then
+// n2 half rows
+double tail_makespan2(int64_t ntx, int64_t B, int64_t F_rows, int64_t n2, int64_t slots, double c, int64_t pre = 0);
 TailPlan tail_plan(int64_t ntx, int64_t B, int64_t ty0, int64_t ty1, int64_t yend, int64_t T, int64_t T2,
-                   int64_t slots, int mode, double c);
+                   int64_t slots, int mode, double c, int64_t pre = 0);
 
 }  // namespace life

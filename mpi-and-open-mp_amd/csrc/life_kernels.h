@@ -113,10 +113,14 @@ struct Extend {
 // Up to 4 disjoint tile regions in one launch; *valu_lane_ops (optional):
 // the modelled VALU lane-ops of the launch as tiled (tstep_valu_per_tile_lane).
 // Regions are in tile coordinates of tile_geom(extended_layout(L, ext), m).
+// `concurrent`: items of another tile launch dispatched just before this one
+// and running beside it (an exchange pass's ring beside its interior); the
+// launch-tail plan of a one-region launch counts them as occupying slots
+// (< 0: no launch-tail split).
 hipError_t launch_tstep(const life_layout &L, const uint8_t *in, uint8_t *out, const TileRegion *r, int nreg,
                         int m, Wrap wrap, hipStream_t s,
                         double *valu_lane_ops = nullptr, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr,
-                        Extend ext = Extend{});
+                        Extend ext = Extend{}, int64_t concurrent = 0);
 // Computes (and caches) the launch-tail plans launch_tstep will use for the
 // whole-shard launches of layout L at m = 1 .. mmax generations (with
 // ext_y: also every deep-halo extension 0 .. K - m), so that a step call

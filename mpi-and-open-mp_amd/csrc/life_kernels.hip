@@ -298,12 +298,14 @@ struct TArgs {
     // ceil((ty1 - ty0) / (64 / G)) banded items
     int32_t gsh;
     int64_t bcol;
-    // tail split (bit, one launch of one full-width region; launch_tstep):
-    // with tail_ntx > 0, workgroups >= tail_first run half-height tiles (R /
-    // 2 rows per wave) over owned rows [tail_y, tail_yend), tail_ntx tile
-    // columns per tile row, the last one banded like the full tiles (gsh <
-    // 6), so the last round of a launch is made of half-length items
-    int64_t tail_first, tail_y, tail_yend, tail_ntx;
+    // tail split (bit, a launch of one region; launch_tstep): with tail_ntx
+    // > 0, workgroups >= tail_first run half-height tiles (R / 2 rows per
+    // wave) over owned rows [tail_y, tail_yend), tile columns [tail_tx0,
+    // tail_tx0 + tail_ntx) per tile row, the last one banded like the full
+    // tiles when it is the banded column (tail_band), so the last round of a
+    // launch is made of half-length items
+    int64_t tail_first, tail_y, tail_yend, tail_ntx, tail_tx0;
+    int32_t tail_band;
     // XCD-aware order (bit, LIFE_XCD_ORDER): workgroups [0, xcd_n) are
     // renumbered so that each XCD (blocks b, b + 8, ... share one) walks a
     // contiguous row-major run of items; 0: dispatch order
@@ -739,18 +741,20 @@ constexpr int bit_wpe(int NW, int R) { return NW == 16 ? (R <= 16 ? 8 : 4) : (R 
 
 // Item i of the tail (TArgs::tail_*): RS rows per wave, tile rows of TS =
 // NW RS - 2m owned rows from owned row tail_y, the last one stopping at
-// tail_yend; tail_ntx - 1 ordinary tiles per tile row, then the banded items
-// of the last tile column (B = 64 >> gsh tile rows each), or tail_ntx tiles
-// per row.  (Round 5's half tiles spanned the last column as full-width
-// tiles; banded they take (64 - o - 2) / 64 fewer lanes there.)
+// tail_yend; tail_ntx - 1 ordinary tiles per tile row from column tail_tx0,
+// then the banded items of the last tile column (B = 64 >> gsh tile rows
+// each), or tail_ntx tiles per row without it.  (Round 5's half tiles spanned
+// the last column as full-width tiles; banded they take (64 - o - 2) / 64
+// fewer lanes there.)
 template <int RS, bool WRAPX, bool WRAPY, int NW>
 __device__ __forceinline__ void tail_item(const TArgs &a, int64_t i, XchB<NW> &xch) {
     const int64_t TS = (int64_t)NW * RS - 2 * a.m, y0 = a.tail_y, yend = a.tail_yend;
     const int64_t rows = (yend - y0 + TS - 1) / TS;
-    const bool band = a.gsh < 6;
+    const bool band = a.tail_band != 0;
     const int64_t ntxs = a.tail_ntx - (band ? 1 : 0), nfull = ntxs * rows;
     if (i < nfull) {
-        tile_body_bit<RS, WRAPX, WRAPY, 0, NW>(a, a.in, a.out, i % ntxs, i / ntxs, xch, 6, 1, y0, yend);
+        tile_body_bit<RS, WRAPX, WRAPY, 0, NW>(a, a.in, a.out, a.tail_tx0 + i % ntxs, i / ntxs, xch, 6, 1, y0,
+                                              yend);
     } else {
         const int64_t B = 64 >> a.gsh, ty = (i - nfull) * B;
         const int nb = (int)(rows - ty < B ? rows - ty : B);
@@ -1961,12 +1965,19 @@ life_layout extended_layout(const life_layout &L, const Extend &ext) {
     return V;
 }
 
-// The tail plan of a full-width bit launch over tile rows [ty0, ty1) of
-// tile_geom(L, m) (launch_tstep; cached by life::tail_plan).
-static TailPlan tail_plan_for(const life_layout &L, const TileGeom &g, int m, int64_t ty0, int64_t ty1) {
+// Bands of the tile columns [tx0, tx1): B tile rows per banded item when
+// the region holds the banded last column, else 1 (no bands).
+static int64_t region_bands(const TileGeom &g, int64_t tx1) { return g.gsh < 6 && tx1 == g.bcol + 1 ? 64 >> g.gsh : 1; }
+
+// The tail plan of a bit launch over tile columns [tx0, tx1) x rows [ty0,
+// ty1) of tile_geom(L, m), beside `pre` items of another launch dispatched
+// just before it (launch_tstep; cached by life::tail_plan).
+static TailPlan tail_plan_for(const life_layout &L, const TileGeom &g, int m, int64_t tx0, int64_t tx1, int64_t ty0,
+                              int64_t ty1, int64_t pre) {
     const int64_t T2 = (int64_t)tile_waves(true) * (temporal_rows(true) / 2) - 2 * (int64_t)tile_ghost(L, m);
-    const int64_t yend = std::min(ty1 * g.rows, L.h), B = g.gsh < 6 ? 64 >> g.gsh : 1;
-    return tail_plan(g.ntx, B, ty0, ty1, yend, g.rows, T2, tstep_bit_slots(), tail_split_mode(), tail_c());
+    const int64_t yend = std::min(ty1 * g.rows, L.h);
+    return tail_plan(tx1 - tx0, region_bands(g, tx1), ty0, ty1, yend, g.rows, T2, tstep_bit_slots(),
+                     tail_split_mode(), tail_c(), pre);
 }
 
 void prewarm_tail_plans(const life_layout &L, int mmax, bool ext_y) {
@@ -1978,13 +1989,13 @@ void prewarm_tail_plans(const life_layout &L, int mmax, bool ext_y) {
             x.y = e;
             const life_layout V = extended_layout(L, x);
             const TileGeom g = tile_geom(V, m);
-            if (g.rows >= 1) (void)tail_plan_for(V, g, m, 0, g.nty);
+            if (g.rows >= 1) (void)tail_plan_for(V, g, m, 0, g.ntx, 0, g.nty, 0);
         }
 }
 
 hipError_t launch_tstep(const life_layout &Lin, const uint8_t *in, uint8_t *out, const TileRegion *r, int nreg,
                         int m, Wrap wrap, hipStream_t s, double *valu_lane_ops, hipEvent_t ev0, hipEvent_t ev1,
-                        Extend ext) {
+                        Extend ext, int64_t concurrent) {
     const int K = Lin.generations_per_exchange;
     const bool bit = is_bit(Lin);
     // m <= 32: the tile's edge lanes absorb at most 32 wrong cells; m <= the
@@ -2022,30 +2033,34 @@ hipError_t launch_tstep(const life_layout &Lin, const uint8_t *in, uint8_t *out,
     }
     if (a.nreg == 0 || m <= 0) return hipSuccess;
     int64_t items = a.first[a.nreg];  // one workgroup per tile (or banded item)
-    a.tail_first = a.tail_y = a.tail_yend = a.tail_ntx = 0;
+    a.tail_first = a.tail_y = a.tail_yend = a.tail_ntx = a.tail_tx0 = 0;
+    a.tail_band = 0;
     const int64_t T2 = (int64_t)tile_waves(bit) * (temporal_rows(bit) / 2) - 2 * (int64_t)tile_ghost(L, m);
-    if (bit && T2 >= 1 && a.nreg == 1 && a.tx0[0] == 0 && a.tx1[0] == g.ntx && tail_split_mode() > 0) {
-        // One full-width region: the whole shard, a deep-halo pass over the
-        // extended shard, or the interior of a row strip (the ring runs
-        // concurrently).  The launch runs items / slots rounds of equal
-        // tiles; a last round under full leaves CUs idle for up to a whole
-        // tile time.  The bottom tile rows are re-tiled as half-height tiles
-        // (banded in the last column like the full tiles, round 6),
-        // dispatched last, so the final round is half-length items on every
-        // slot (life::tail_plan).  The byte tiles (2 per CU, 32 ghost rows: a
-        // third of a half tile) lost 3-4 % with half tiles (profiles/r02/r2z)
-        // and keep whole tiles.
-        const int64_t ty0 = a.ty0[0], ty1 = a.ty1[0], yend = std::min(ty1 * g.rows, L.h);
-        const int64_t B = g.gsh < 6 ? 64 >> g.gsh : 1;
-        const TailPlan p = tail_plan_for(L, g, m, ty0, ty1);
+    if (bit && T2 >= 1 && a.nreg == 1 && tail_split_mode() > 0 && concurrent >= 0) {
+        // One region: the whole shard, a deep-halo pass over the extended
+        // shard, a row strip's interior, or (round 6) the interior of an
+        // exchange pass beside its ring (`concurrent` = the ring's items,
+        // dispatched just before it on another stream).  The launch runs
+        // items / slots rounds of equal tiles; a last round under full leaves
+        // CUs idle for up to a whole tile time.  The bottom tile rows are
+        // re-tiled as half-height tiles (banded in the last column like the
+        // full tiles, round 6), dispatched last, so the final round is
+        // half-length items on every slot (life::tail_plan).  The byte tiles
+        // (2 per CU, 32 ghost rows: a third of a half tile) lost 3-4 % with
+        // half tiles (profiles/r02/r2z) and keep whole tiles.
+        const int64_t tx0 = a.tx0[0], tx1 = a.tx1[0], ty0 = a.ty0[0], ty1 = a.ty1[0];
+        const int64_t yend = std::min(ty1 * g.rows, L.h), B = region_bands(g, tx1);
+        const TailPlan p = tail_plan_for(L, g, m, tx0, tx1, ty0, ty1, concurrent);
         if (p.F < ty1 && p.F >= ty0) {
             a.ty1[0] = p.F;
-            a.first[1] = region_items(g, TileRegion{0, g.ntx, ty0, p.F});
+            a.first[1] = region_items(g, TileRegion{tx0, tx1, ty0, p.F});
             a.tail_first = a.first[1];
             a.tail_y = p.F * g.rows;
             a.tail_yend = yend;
-            a.tail_ntx = g.ntx;
-            items = a.tail_first + tail_row_items(g.ntx, B, p.n2);
+            a.tail_ntx = tx1 - tx0;
+            a.tail_tx0 = tx0;
+            a.tail_band = B > 1 ? 1 : 0;
+            items = a.tail_first + tail_row_items(tx1 - tx0, B, p.n2);
         }
     }
     const bool split = a.tail_ntx > 0;

@@ -346,19 +346,20 @@ struct SlotGroups {
 };
 
 struct TailKey {
-    int64_t ntx, B, ty0, ty1, yend, T, T2, slots;
+    int64_t ntx, B, ty0, ty1, yend, T, T2, slots, pre;
     int mode;
     double c;
     bool operator==(const TailKey &o) const {
         return ntx == o.ntx && B == o.B && ty0 == o.ty0 && ty1 == o.ty1 && yend == o.yend && T == o.T && T2 == o.T2 &&
-               slots == o.slots && mode == o.mode && c == o.c;
+               slots == o.slots && pre == o.pre && mode == o.mode && c == o.c;
     }
 };
 }  // namespace
 
-double life::tail_makespan2(int64_t ntx, int64_t B, int64_t F_rows, int64_t n2, int64_t slots, double c) {
+double life::tail_makespan2(int64_t ntx, int64_t B, int64_t F_rows, int64_t n2, int64_t slots, double c,
+                            int64_t pre) {
     if (slots < 1) return 0.0;
-    const int64_t nf = tail_row_items(ntx, B, F_rows);
+    const int64_t nf = (pre > 0 ? pre : 0) + tail_row_items(ntx, B, F_rows);
     const int64_t r = nf / slots, rem = nf % slots;
     SlotGroups g;
     g.add((double)r, slots - rem);
@@ -368,19 +369,20 @@ double life::tail_makespan2(int64_t ntx, int64_t B, int64_t F_rows, int64_t n2, 
 }
 
 life::TailPlan life::tail_plan(int64_t ntx, int64_t B, int64_t ty0, int64_t ty1, int64_t yend, int64_t T,
-                               int64_t T2, int64_t slots, int mode, double c) {
+                               int64_t T2, int64_t slots, int mode, double c, int64_t pre) {
     TailPlan none;
     none.F = ty1;
-    if (ntx < 1 || ty1 <= ty0 || T < 1 || T2 < 1 || slots < 1 || mode < 1 || mode > 2) return none;
-    const int64_t nall = tail_row_items(ntx, B, ty1 - ty0);
-    none.makespan = tail_makespan2(ntx, B, ty1 - ty0, 0, slots, c);
+    if (ntx < 1 || ty1 <= ty0 || T < 1 || T2 < 1 || slots < 1 || mode < 1 || mode > 2 || pre < 0) return none;
+    // the launch shares the slots with `pre` items dispatched before it
+    const int64_t nall = pre + tail_row_items(ntx, B, ty1 - ty0);
+    none.makespan = tail_makespan2(ntx, B, ty1 - ty0, 0, slots, c, pre);
     // Whole rounds: nothing to fill.  One round or less: the model's slots are
     // not independent there (a CU's three slots share its SIMDs, and a lone
     // tile runs faster), so it is not trusted to re-tile an underfilled launch.
     if (nall <= slots || nall % slots == 0) return none;
     static std::mutex mu;
     static std::vector<std::pair<TailKey, TailPlan>> cache;
-    const TailKey key{ntx, B, ty0, ty1, yend, T, T2, slots, mode, c};
+    const TailKey key{ntx, B, ty0, ty1, yend, T, T2, slots, pre, mode, c};
     {
         std::lock_guard<std::mutex> lk(mu);
         for (const auto &e : cache)
@@ -400,14 +402,14 @@ life::TailPlan life::tail_plan(int64_t ntx, int64_t B, int64_t ty0, int64_t ty1,
             if (q < ty1 - ty0) {
                 best.F = ty1 - q;
                 best.n2 = halves(best.F);
-                best.makespan = tail_makespan2(ntx, B, best.F - ty0, best.n2, slots, c);
+                best.makespan = tail_makespan2(ntx, B, best.F - ty0, best.n2, slots, c, pre);
             }
         }
     } else {
         // every split point (ties keep more full tiles)
         for (int64_t F = ty1 - 1; F >= ty0; --F) {
             const int64_t n2 = halves(F);
-            const double t = tail_makespan2(ntx, B, F - ty0, n2, slots, c);
+            const double t = tail_makespan2(ntx, B, F - ty0, n2, slots, c, pre);
             if (t < best.makespan - 1e-9) {
                 best.F = F;
                 best.n2 = n2;

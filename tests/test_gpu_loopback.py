@@ -169,3 +169,27 @@ def test_loopback_one_axis(gpu, oracle, nx, ny, gens, kernel, rccl, axes):
         life.step(split)
         life.step(gens - split)
         np.testing.assert_array_equal(life.gather(), want)
+
+
+@pytest.mark.parametrize("axes", [1, 2], ids=["xy", "x_only"])
+@pytest.mark.parametrize("shape", [(16384, 32768), (32768, 16384)])
+def test_exchange_pass_interior_tail(gpu, shape, axes):
+    """Round 6: the exchange pass's interior launch takes the banded
+    half-height tail too, planned with the ring's tiles (dispatched just
+    before it on the other stream) counted as holding their slots --
+    configs[3]'s N = 8 block: 567 interior tiles beside 247 ring tiles.  The
+    RCCL-loopback run (several exchange blocks, both axes or x only) against
+    the same grid run unpartitioned (itself pinned to the oracle by
+    test_gpu_fullsize's banded-tail band checks), by census."""
+    nx, ny = shape
+    gens = 77
+    with gpu.Life(nx, ny, kernel="bit", flow=0) as life:
+        life.fill_random(9, 0.5)
+        life.step(gens)
+        want = (life.checksum(), life.live_count())
+    with _make(gpu, nx, ny, "bit", "rank") as life:
+        life.fill_random(9, 0.5)
+        life.configure(gpu.OPT_LOOPBACK, axes)
+        life.step(30)
+        life.step(gens - 30)
+        assert (life.checksum(), life.live_count()) == want
