@@ -6,7 +6,9 @@
 # 2.53 at 32768^2.  Expectation: RCCL-loopback lines 16384x32768 +5-8 %,
 # 32768^2 +3-6 %, 65536^2 +0-2 %; parity green.  The unpartitioned lines of
 # the same shapes and steps alternate with them, so the scaling tables can be
-# rebuilt from this job if it is kept (scripts/scaling_table.py).
+# rebuilt from this job if it is kept (scripts/scaling_table.py).  (The
+# whole GPU suite and the trace run in the next job: one call stays under
+# 20 minutes.)
 cd "$GRAFT_REPO_ROOT" || exit 1
 R=$GRAFT_REPO_ROOT
 O=gpurun_out/r06/f; mkdir -p $O
@@ -35,8 +37,4 @@ for i in 1 2; do
     LIFE_INTERIOR_TAIL=$t $S 150 $O/l992_16384x32768_xy_it${t}_$i.log $L --shape 16384x32768 --loopback-axes xy || exit $?
   done
 done
-cd /tmp && export TMPDIR=/tmp && cd $R
-$S 150 $O/trace_loop16384.log timeout -s KILL 140 rocprofv3 --kernel-trace --stats -d $O/trace_loop16384 -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --rank-mode --loopback --no-parity --shape 16384x32768 --steps 96 --warmup 32 || exit $?
-$S 1150 $O/pytest.log $T tests -m gpu || exit $?
-grep -q " passed" $O/pytest.log && ! grep -q -E "[0-9]+ (failed|error)" $O/pytest.log || exit 1
 echo done
