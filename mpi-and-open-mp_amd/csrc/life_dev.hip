@@ -647,14 +647,18 @@ int launch_tiles(life_dev *d, Shard &s, const life::TileRegion *r, int nreg, int
     return LIFE_OK;
 }
 
-// LIFE_INTERIOR_TAIL (0/1, default 1, read once; A/B knob): the exchange
-// pass's interior launch takes the banded half-height tail, planned with the
-// ring's tiles counted as holding their slots (round 6); 0: no tail split
-// for it (round 5).
+// LIFE_INTERIOR_TAIL (0/1, default 0, read once; A/B knob): 1 = the
+// exchange pass's interior launch takes the banded half-height tail, planned
+// with the ring's tiles counted as holding their slots; 0 = as in round 5,
+// only a full-width interior (a row strip's) splits, planned alone.  Off by default: in
+// r06f's ABAB loopback lines it shortened the interior by 4-9 % but the halo
+// behind the ring was exposed longer by as much (the half tiles take the
+// slots the RCCL kernels would get once the ring drains), so
+// the block did not get shorter.
 static bool interior_tail() {
     static const bool v = [] {
         const char *e = getenv("LIFE_INTERIOR_TAIL");
-        return e ? atoi(e) != 0 : true;
+        return e ? atoi(e) != 0 : false;
     }();
     return v;
 }
@@ -845,11 +849,13 @@ int generation_block(life_dev *d, int m, bool last) {
         const int64_t items = life::region_items(g, inner) + ring_items;
         halo_side[si] = carry_on_halo_side(items, life::tile_slots(s.lay)) ? 1 : 0;
         if (pe[si]) HIPCHK(hipEventRecord(pe[si]->int0, s.stream2));
-        // the interior's launch-tail plan counts the ring's tiles, dispatched
-        // just before it, as holding their slots (round 6: 16384 x 32768's 584
-        // interior tiles beside 249 ring tiles are one round plus a tail)
-        if (rb > ra && cb > ca)
-            CHK(launch_tiles(d, s, &inner, 1, m, true, s.stream2, life::Extend{}, interior_tail() ? ring_items : -1));
+        // LIFE_INTERIOR_TAIL=1: the interior's launch-tail plan counts the
+        // ring's tiles, dispatched just before it, as holding their slots
+        // (16384 x 32768's 584 interior tiles beside 249 ring tiles are one
+        // round plus a tail); default: only a row strip's full-width interior
+        // splits its tail, planned alone (round 5)
+        const int64_t conc = interior_tail() ? ring_items : (ca == 0 && cb == NX ? 0 : -1);
+        if (rb > ra && cb > ca) CHK(launch_tiles(d, s, &inner, 1, m, true, s.stream2, life::Extend{}, conc));
         if (pe[si]) HIPCHK(hipEventRecord(pe[si]->int1, s.stream2));
     }
     if (!(rx || ry)) {

@@ -1,8 +1,8 @@
 #!/bin/bash
-# r06g: validation after the exchange-pass interior tail (r06f): smoke, the
-# driver-shaped line, a kernel trace of the 16384x32768 RCCL loopback (the
-# exchange pass's interior with its banded half tail beside the ring), the
-# whole GPU suite.  Expectation: all green.
+# r06g: validation after r06f (the exchange-pass interior tail measured flat,
+# now off by default): smoke, the driver-shaped line, a kernel trace of the
+# 16384x32768 RCCL loopback, the whole GPU suite (incl. the interior tail
+# both ways).  Expectation: all green.
 cd "$GRAFT_REPO_ROOT" || exit 1
 R=$GRAFT_REPO_ROOT
 O=gpurun_out/r06/g; mkdir -p $O

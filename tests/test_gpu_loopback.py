@@ -171,25 +171,45 @@ def test_loopback_one_axis(gpu, oracle, nx, ny, gens, kernel, rccl, axes):
         np.testing.assert_array_equal(life.gather(), want)
 
 
-@pytest.mark.parametrize("axes", [1, 2], ids=["xy", "x_only"])
-@pytest.mark.parametrize("shape", [(16384, 32768), (32768, 16384)])
-def test_exchange_pass_interior_tail(gpu, shape, axes):
-    """Round 6: the exchange pass's interior launch takes the banded
-    half-height tail too, planned with the ring's tiles (dispatched just
-    before it on the other stream) counted as holding their slots --
-    configs[3]'s N = 8 block: 567 interior tiles beside 247 ring tiles.  The
-    RCCL-loopback run (several exchange blocks, both axes or x only) against
-    the same grid run unpartitioned (itself pinned to the oracle by
-    test_gpu_fullsize's banded-tail band checks), by census."""
-    nx, ny = shape
-    gens = 77
-    with gpu.Life(nx, ny, kernel="bit", flow=0) as life:
+_INTERIOR_TAIL = r"""
+import sys
+sys.path.insert(0, {pkg!r})
+import life_mi355x as lm
+for nx, ny in ((16384, 32768), (32768, 16384)):
+    with lm.Life(nx, ny, kernel="bit", flow=0) as life:
         life.fill_random(9, 0.5)
-        life.step(gens)
+        life.step(77)
         want = (life.checksum(), life.live_count())
-    with _make(gpu, nx, ny, "bit", "rank") as life:
-        life.fill_random(9, 0.5)
-        life.configure(gpu.OPT_LOOPBACK, axes)
-        life.step(30)
-        life.step(gens - 30)
-        assert (life.checksum(), life.live_count()) == want
+    for axes in (1, 2):
+        with lm.Life.for_rank(nx, ny, 0, 1, lm.unique_id(), 0, kernel="bit") as life:
+            life.fill_random(9, 0.5)
+            life.configure(lm.OPT_LOOPBACK, axes)
+            life.step(30)
+            life.step(47)
+            got = (life.checksum(), life.live_count())
+            assert got == want, (nx, ny, axes, got, want)
+print("INTERIOR_TAIL_OK", flush=True)
+"""
+
+
+@pytest.mark.parametrize("tail", ["0", "1"], ids=["default", "interior_tail"])
+def test_exchange_pass_interior_tail(gpu, tail):
+    """Round 6: with LIFE_INTERIOR_TAIL=1 the exchange pass's interior launch
+    takes the banded half-height tail too, planned with the ring's tiles
+    (dispatched just before it on the other stream) counted as holding their
+    slots -- configs[3]'s N = 8 block: 567 interior tiles beside 247 ring
+    tiles; off by default.  Both settings (the knob is read
+    once per process, hence the subprocess): the RCCL-loopback run (several
+    exchange blocks, both axes or x only) against the same grid run
+    unpartitioned (itself pinned to the oracle by test_gpu_fullsize's
+    banded-tail band checks), by census."""
+    import os
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+
+    env = dict(os.environ, LIFE_INTERIOR_TAIL=tail)
+    out = subprocess.run([sys.executable, "-c", _INTERIOR_TAIL.format(pkg=os.path.join(ROOT, "mpi-and-open-mp_amd"))],
+                         env=env, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0 and "INTERIOR_TAIL_OK" in out.stdout, out.stdout + out.stderr
