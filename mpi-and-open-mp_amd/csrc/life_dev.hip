@@ -86,7 +86,7 @@ struct Shard {
     hipStream_t stream = nullptr;   // compute: whole-block kernels, boundary ring
     hipStream_t stream2 = nullptr;  // compute: interior, concurrent with ring + halo
     hipStream_t comm_stream = nullptr;
-    hipEvent_t ev_ring = nullptr, ev_halo = nullptr, ev_sync = nullptr, ev_int = nullptr, ev_join = nullptr;
+    hipEvent_t ev_halo = nullptr, ev_sync = nullptr, ev_int = nullptr;
     hipEvent_t ev_entry = nullptr;  // life_dev_step entry fence (see there)
     // device span of the last step call (timing on): own_a / own_b recorded at
     // the call's two ends, or the kTimeCall pair borrowed (span_a / span_b)
@@ -152,6 +152,17 @@ static const double kFlowAutoRounds = [] {
 static const bool kEnvDeepHalo = [] {
     const char *e = getenv("LIFE_DEEP_HALO");
     return e ? atoi(e) != 0 : true;
+}();
+// LIFE_SYNC_EVENTS (measurement knob, read at load): the flags of the events
+// that order a shard's ring / halo stream and its interior stream on one
+// device -- 0 hipEventDisableTiming (system-scope release and acquire when
+// recorded, HIP's default), 1 + hipEventDisableSystemFence, 2 +
+// hipEventReleaseToDevice.
+static const unsigned kSyncEventFlags = [] {
+    const char *e = getenv("LIFE_SYNC_EVENTS");
+    const int v = e ? atoi(e) : 0;
+    return (unsigned)hipEventDisableTiming |
+           (v == 1 ? (unsigned)hipEventDisableSystemFence : v == 2 ? (unsigned)hipEventReleaseToDevice : 0u);
 }();
 static int default_block_gens(int kernel) {
     return kEnvBlockGens ? kEnvBlockGens : (kernel == LIFE_KERNEL_BIT ? 12 : 32);
@@ -268,12 +279,13 @@ int shard_alloc(life_dev *d, Shard &s) {
         HIPCHK(hipMalloc(&s.buf[i], bytes));
         HIPCHK(hipMemsetAsync(s.buf[i], fill, bytes, s.stream));
     }
-    HIPCHK(hipEventCreateWithFlags(&s.ev_int, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&s.ev_join, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&s.ev_ring, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&s.ev_halo, hipEventDisableTiming));
+    // ev_int / ev_halo / ev_entry order the shard's own streams on its own
+    // device (kSyncEventFlags); ev_sync orders other shards' streams, maybe
+    // on other devices, and keeps the system-scope fence
+    HIPCHK(hipEventCreateWithFlags(&s.ev_int, kSyncEventFlags));
+    HIPCHK(hipEventCreateWithFlags(&s.ev_halo, kSyncEventFlags));
     HIPCHK(hipEventCreateWithFlags(&s.ev_sync, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&s.ev_entry, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&s.ev_entry, kSyncEventFlags));
     const size_t col_bytes = (size_t)life::column_stage_bytes(s.lay);
     HIPCHK(hipMalloc(&s.col_send, col_bytes));
     HIPCHK(hipMalloc(&s.col_recv, col_bytes));
@@ -311,7 +323,7 @@ void shard_free(Shard &s) {
     if (s.flow) (void)hipFree(s.flow);
     if (s.d_count) (void)hipFree(s.d_count);
     if (s.h_count) (void)hipHostFree(s.h_count);
-    for (hipEvent_t e : {s.ev_ring, s.ev_halo, s.ev_sync, s.ev_int, s.ev_join, s.ev_entry, s.own_a, s.own_b})
+    for (hipEvent_t e : {s.ev_halo, s.ev_sync, s.ev_int, s.ev_entry, s.own_a, s.own_b})
         if (e) (void)hipEventDestroy(e);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     if (s.stream2) (void)hipStreamDestroy(s.stream2);
