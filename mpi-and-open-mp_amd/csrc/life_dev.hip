@@ -153,17 +153,6 @@ static const bool kEnvDeepHalo = [] {
     const char *e = getenv("LIFE_DEEP_HALO");
     return e ? atoi(e) != 0 : true;
 }();
-// LIFE_SYNC_EVENTS (measurement knob, read at load): the flags of the events
-// that order a shard's ring / halo stream and its interior stream on one
-// device -- 0 hipEventDisableTiming (system-scope release and acquire when
-// recorded, HIP's default), 1 + hipEventDisableSystemFence, 2 +
-// hipEventReleaseToDevice.
-static const unsigned kSyncEventFlags = [] {
-    const char *e = getenv("LIFE_SYNC_EVENTS");
-    const int v = e ? atoi(e) : 0;
-    return (unsigned)hipEventDisableTiming |
-           (v == 1 ? (unsigned)hipEventDisableSystemFence : v == 2 ? (unsigned)hipEventReleaseToDevice : 0u);
-}();
 static int default_block_gens(int kernel) {
     return kEnvBlockGens ? kEnvBlockGens : (kernel == LIFE_KERNEL_BIT ? 12 : 32);
 }
@@ -279,13 +268,12 @@ int shard_alloc(life_dev *d, Shard &s) {
         HIPCHK(hipMalloc(&s.buf[i], bytes));
         HIPCHK(hipMemsetAsync(s.buf[i], fill, bytes, s.stream));
     }
-    // ev_int / ev_halo / ev_entry order the shard's own streams on its own
-    // device (kSyncEventFlags); ev_sync orders other shards' streams, maybe
-    // on other devices, and keeps the system-scope fence
-    HIPCHK(hipEventCreateWithFlags(&s.ev_int, kSyncEventFlags));
-    HIPCHK(hipEventCreateWithFlags(&s.ev_halo, kSyncEventFlags));
+    // (device-scope forms of these events, hipEventDisableSystemFence /
+    // hipEventReleaseToDevice, measured flat: profiles/r06/h)
+    HIPCHK(hipEventCreateWithFlags(&s.ev_int, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&s.ev_halo, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&s.ev_sync, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&s.ev_entry, kSyncEventFlags));
+    HIPCHK(hipEventCreateWithFlags(&s.ev_entry, hipEventDisableTiming));
     const size_t col_bytes = (size_t)life::column_stage_bytes(s.lay);
     HIPCHK(hipMalloc(&s.col_send, col_bytes));
     HIPCHK(hipMalloc(&s.col_recv, col_bytes));
