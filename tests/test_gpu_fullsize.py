@@ -260,3 +260,60 @@ def test_c3_1000_generations_band_vs_oracle(gpu, oracle):
     want = oracle.life_run(band, gens, threads=_threads())[:, margin:margin + 2 * half]
     for kernel, g in got.items():
         np.testing.assert_array_equal(g, want, err_msg=f"{kernel} after {gens} generations")
+
+
+_SPLIT_SHAPES = r"""
+import json, sys
+sys.path.insert(0, {pkg!r})
+import life_mi355x as lm
+out = []
+for nx, ny, bmax, gens, seed in {cases!r}:
+    with lm.Life(nx, ny, kernel="bit", flow=0) as life:
+        life.configure(lm.OPT_BLOCK_GENS, bmax)
+        life.fill_random(seed, 0.5)
+        life.set_timing(True)
+        life.step(gens)
+        assert life.last_path() == "tiles"
+        out.append([life.checksum(), life.live_count(), life.kernel_work()[1]])
+print("CENSUS " + json.dumps(out), flush=True)
+"""
+
+
+def test_tail_split_equals_unsplit_random_shapes(gpu):
+    """The launch-tail split (banded half-height tiles, life::tail_plan) on
+    shapes drawn at random -- widths of whole 64-cell pairs that are not a
+    multiple of the 62-pair tile (band widths of the last tile column from 2
+    to 64 lanes), odd heights, launches of 1-6 rounds, pass lengths 5-12 --
+    equals the same runs with the split off (LIFE_TAIL_SPLIT=0: whole tiles
+    only, the path the oracle tests pin at every size), by census.  Both
+    settings run in subprocesses (the knob is read once per process)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+
+    rng = np.random.default_rng(6)
+    cases = []
+    while len(cases) < 10:
+        nx = 64 * int(rng.integers(63, 625))  # whole pairs: a width that is not wraps through its own apron (no split)
+        ny = int(rng.integers(12000, 60000)) | 1
+        bmax = int(rng.integers(5, 13))
+        rounds = -(-nx // 3968) * -(-ny // (192 - 2 * bmax)) / 768  # tile_geom, roughly
+        if nx * ny > 1_200_000_000 or not 1.02 < rounds < 6 or rounds % 1 < 0.05:
+            continue  # a launch the planner may split: over one round, not whole rounds
+        cases.append((nx, ny, bmax, int(rng.integers(bmax, 3 * bmax + 1)), int(rng.integers(1, 1000))))
+    script = _SPLIT_SHAPES.format(pkg=os.path.join(ROOT, "mpi-and-open-mp_amd"), cases=cases)
+    res = {}
+    for mode in ("0", "2"):
+        env = dict(os.environ, LIFE_TAIL_SPLIT=mode)
+        out = subprocess.run([sys.executable, "-c", script], env=env, capture_output=True, text=True, timeout=110)
+        assert out.returncode == 0, out.stdout + out.stderr
+        res[mode] = json.loads(out.stdout.split("CENSUS ", 1)[1])
+    census = [[r[:2] for r in res[m]] for m in ("0", "2")]
+    assert census[0] == census[1], list(zip(cases, *census))
+    # the issued-work model books half tiles as half: the runs the planner
+    # split show up as a different VALU count
+    split = sum(a[2] != b[2] for a, b in zip(res["0"], res["2"]))
+    assert split >= 5, (split, res)
