@@ -7,13 +7,11 @@
 # rounds (8.67 against 9.00), m = 10 ~8.45 against 8.59.  Expectation:
 # 16384x32768 +25-40 %, 32768^2 tiles +10-15 %, 65536^2 992 gens +3 %,
 # driver line +1-2 %; the dataflow instance spills at 26 rows (24-60 B
-# scratch): flow lines slower.  Parity subset under 26 first.
+# scratch): flow lines slower.  Parity subset under 26 after the lines.
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/r06/k; mkdir -p $O
 S=scripts/gpu_step.sh
 T="python -u -m pytest -x -q --timeout 600 --timeout-method thread -p no:cacheprovider"
-LIFE_TEMPORAL_ROWS=26 $S 600 $O/pytest26.log $T tests/test_gpu_fullsize.py tests/test_gpu_parity.py tests/test_gpu_loopback.py -m gpu -k "band or tail or driver_shape or random_shapes or parity or loopback or deep" || exit $?
-grep -q " passed" $O/pytest26.log && ! grep -q -E "[0-9]+ (failed|error)" $O/pytest26.log || exit 1
 U="python -u bench.py --no-cpu-baseline"
 L="python -u bench.py --no-cpu-baseline --rank-mode --loopback --no-parity"
 for i in 1 2; do
@@ -30,4 +28,6 @@ done
 for r in 24 26; do
   LIFE_TEMPORAL_ROWS=$r $S 150 $O/u992_32768_flow_r${r}.log $U --shape 32768x32768 --flow 1 || exit $?
 done
+LIFE_TEMPORAL_ROWS=26 $S 600 $O/pytest26.log $T tests/test_gpu_fullsize.py tests/test_gpu_parity.py tests/test_gpu_loopback.py -m gpu -k "band or tail or driver_shape or random_shapes or parity or loopback or deep" || exit $?
+grep -q " passed" $O/pytest26.log && ! grep -q -E "[0-9]+ (failed|error)" $O/pytest26.log || exit 1
 echo done
