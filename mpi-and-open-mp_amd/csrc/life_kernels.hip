@@ -737,7 +737,7 @@ __device__ __forceinline__ void tile_body_byte(const TArgs &a, const uint8_t *in
 // Waves per SIMD the bit tiles are compiled for (the VGPR budget): 3 tiles
 // of 8 waves or 2 of 12 per CU at <= 80 VGPRs; 16-wave tiles: 2 per CU at 64
 // (R = 16) or 1 at 128.
-constexpr int bit_wpe(int NW, int R) { return NW == 16 ? (R <= 16 ? 8 : 4) : (R <= 26 ? 6 : 4); }
+constexpr int bit_wpe(int NW, int R) { return NW == 16 ? (R <= 16 ? 8 : 4) : (R <= 24 ? 6 : 4); }
 
 // Item i of the tail (TArgs::tail_*): RS rows per wave, tile rows of TS =
 // NW RS - 2m owned rows from owned row tail_y, the last one stopping at
@@ -1662,9 +1662,9 @@ Tunings &tunings() {
 // 0.96-0.99 of 24x8, profiles/r05/a).
 // (byte 64-row tiles, round 5: 61.3 vs 60.5 T at 65536^2, 48.1 vs 50.0 T at
 // 32768^2 -- flat, removed; profiles/r05/g)
-bool temporal_rows_ok(bool bit, int nr) { return bit ? (nr == 16 || nr == 24 || nr == 26) : (nr == 32 || nr == 48); }
+bool temporal_rows_ok(bool bit, int nr) { return bit ? (nr == 16 || nr == 24) : (nr == 32 || nr == 48); }
 // bit tile shapes with a kernel instance (pair rows R x waves NW)
-bool bit_shape_ok(int R, int NW) { return NW == 8 && (R == 16 || R == 24 || R == 26); }
+bool bit_shape_ok(int R, int NW) { return NW == 8 && (R == 16 || R == 24); }
 }  // namespace
 
 StepTuning step_tuning(bool bit) { return tunings().t[bit ? 1 : 0]; }
@@ -1812,7 +1812,7 @@ const void *bit_fn(Wrap wrap) {
 }
 
 // the bit tile shape's instances: per-launch tiles and the occupancy probe
-#define LIFE_BIT_SHAPES(X) X(24, 8) X(16, 8) X(26, 8)
+#define LIFE_BIT_SHAPES(X) X(24, 8) X(16, 8)
 const void *bit_k(Wrap wrap) {
     const int R = temporal_rows(true), NW = tile_waves(true);
 #define LIFE_BIT_CASE(r, nw) \

@@ -138,8 +138,8 @@ def test_timing_stats(gpu, kernel, nx, gens, flow):
         assert (valu > 0) == temporal
         if temporal:  # ceil(4096 / (NW waves x R rows - 2m)) tile rows of 62-lane tiles, 64 lanes each
             R, NW = gpu.TEMPORAL_ROWS[kernel], gpu.TILE_WAVES[kernel]
-            if kernel == "bit" and os.environ.get("LIFE_TEMPORAL_ROWS") in ("16", "26"):
-                R = int(os.environ["LIFE_TEMPORAL_ROWS"])  # the A/B tile heights (life_kernels.hip)
+            if kernel == "bit" and os.environ.get("LIFE_TEMPORAL_ROWS") == "16":
+                R = int(os.environ["LIFE_TEMPORAL_ROWS"])  # the A/B tile height (life_kernels.hip)
             want = 0
             for m in sizes:
                 ghost = m if kernel == "bit" else K  # byte tiles: compile-time ghost depth K
